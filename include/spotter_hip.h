@@ -1,0 +1,146 @@
+/*
+ * spotter_hip.h — C-ABI of libspotter_hip.so, the MI355X (gfx950) kernels of
+ * the RT-DETRv2 /detect hot path.
+ *
+ * The reference has no C-ABI: its hot path is the duck-typed HF interface
+ * AmenitiesDetector calls (apps/spotter/src/spotter/serve.py:98-117):
+ *   processor(images=PIL, return_tensors="pt")           -> sp_preprocess_u8
+ *   model(**inputs) (RTDetrV2ForObjectDetection.forward) -> sp_conv2d, sp_maxpool3x3s2,
+ *        sp_avgpool2x2_ceil, sp_upsample2x_nearest, sp_layernorm, sp_attention,
+ *        sp_msda, sp_topk_rows, sp_gather_rows, sp_ref_init, sp_box_refine
+ *   processor.post_process_object_detection(...)         -> sp_postprocess
+ * (HF sources: transformers/models/rt_detr/image_processing_pil_rt_detr.py:
+ * 451-462, 508-578; transformers/models/rt_detr_v2/modeling_rt_detr_v2.py:
+ * 44-225, 1461-1656, 1797-1881.) spotter_amd/ (Python) implements that
+ * interface on top of these entry points; INTEGRATION.md shows the binding.
+ *
+ * Conventions: plain device pointers (fp32 unless stated), sizes in elements,
+ * `stream` is a hipStream_t (NULL = default stream). Every call is async on
+ * `stream`, allocates nothing and is safe to capture in a hipGraph (except the
+ * first sp_preprocess_u8 per (in, out) size, which uploads its coefficient
+ * table). Return: 0 ok, >0 hipError_t, <0 argument error; the message is in
+ * sp_last_error() (thread-local). No C++ exception crosses the ABI.
+ */
+#ifndef SPOTTER_HIP_H
+#define SPOTTER_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SP_ABI_VERSION 1
+
+enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
+
+/* One uint8 RGB HWC image in device memory. */
+typedef struct {
+  const uint8_t* data;
+  int32_t height, width;
+  int32_t row_stride; /* bytes between rows (>= 3*width) */
+} sp_image_u8;
+
+/*
+ * Implicit-GEMM convolution / linear layer on fp32 MFMA (v_mfma_f32_32x32x2f32):
+ *   out[m, n] = act( (Σ_k A[m, k] · W[n, k]) · row_scale[m % row_period] · scale[n]
+ *                    + shift[n] + res1[m, n] ) + res2[m, n]
+ * A is NHWC: pixel (b, y, x) starts at A + ((b*H + y)*W + x)*lda, channels [0, Cin).
+ * A2 (optional) is added to A element-wise on load (same indexing, lda2).
+ * W is [Cout][KH][KW][Cin] (k contiguous). m = (b*Ho + oy)*Wo + ox.
+ * Output row m goes to C + (m / out_rows_per_group)*out_group_stride + (m % out_rows_per_group)*ldc
+ * (out_rows_per_group = 0 means M, i.e. plain row-major with ldc).
+ * res1/res2 rows use (m*ldr). Linear layers: N=1, H=1, W=rows, KH=KW=1.
+ * Corresponds to nn.Conv2d + (Frozen)BatchNorm2d + activation (+ residual)
+ * (RN:38-68, RN:225-231, M2:817-835) and nn.Linear (+ activation).
+ */
+typedef struct {
+  const float* A; int64_t lda;
+  const float* A2; int64_t lda2;
+  int32_t N, H, W, Cin;
+  int32_t KH, KW, stride, pad;
+  int32_t Ho, Wo;
+  const float* Wt; int32_t Cout;
+  const float* scale;     /* [Cout] or NULL (1) */
+  const float* shift;     /* [Cout] or NULL (0) */
+  const float* row_scale; int32_t row_period; /* NULL or [row_period] */
+  const float* res1; int64_t ldr1;
+  int32_t act;
+  const float* res2; int64_t ldr2;
+  float* C; int64_t ldc;
+  int32_t out_rows_per_group; int64_t out_group_stride;
+} sp_conv_desc;
+
+/*
+ * Multi-scale deformable attention v2 core + softmax + sampling-location math
+ * (M2:166-225, M2:44-115, method "default"), one decoder layer.
+ *   value   [B, S, ld_value] rows, head h channel c at column value_col + h*Dh + c
+ *   off_aw  [B*Q, ld_off_aw]: columns [0, H*L*P*2) sampling offsets (h, l, p, xy),
+ *           then [H*L*P*2, +H*L*P) attention logits (h, l*P + p)
+ *   ref     [B*Q, 4] reference boxes (cx, cy, w, h) in (0, 1)
+ *   out     [B*Q, ld_out] with column h*Dh + c
+ */
+typedef struct {
+  const float* value; int64_t ld_value; int32_t value_col;
+  const float* off_aw; int64_t ld_off_aw;
+  const float* ref;
+  float* out; int64_t ld_out;
+  int32_t B, S, Q, heads, head_dim, levels, points;
+  int32_t level_h[4], level_w[4], level_start[4];
+  float offset_scale;
+} sp_msda_desc;
+
+int sp_abi_version(void);
+const char* sp_last_error(void);
+int sp_device_init(int device);
+
+/* RTDetrImageProcessorPil resize (PIL BILINEAR, bit-exact) + rescale 1/255 + HWC→CHW
+ * (IPP:451-462, IT:118-122, IT:367). out: [n, 3, out_h, out_w] fp32. */
+int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int out_w, float* out,
+                     void* stream);
+
+int sp_conv2d(const sp_conv_desc* d, void* stream);
+
+/* NCHW → NHWC (pixel_values layout of the processor contract → conv layout). */
+int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* stream);
+/* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). */
+int sp_maxpool3x3s2(const float* x, float* y, int n, int h, int w, int c, void* stream);
+/* nn.AvgPool2d(2, 2, 0, ceil_mode=True) on NHWC (RN:150, RN:202). */
+int sp_avgpool2x2_ceil(const float* x, float* y, int n, int h, int w, int c, void* stream);
+/* F.interpolate(scale_factor=2, mode="nearest") into a channel slice (M2:1192). */
+int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, int n, int h,
+                          int w, int c, void* stream);
+/* nn.LayerNorm over the last dim (d <= 1024). */
+int sp_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float* y,
+                 int64_t ldy, int rows, int d, float eps, void* stream);
+/* softmax(Q Kᵀ · scale) V per (batch, head); Q/K/V rows [batch*n, ld], head h at col h*dh. */
+int sp_attention(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                 int64_t ldv, float* o, int64_t ldo, int batch, int n, int heads, int dh,
+                 float scale, void* stream);
+int sp_msda(const sp_msda_desc* d, void* stream);
+/* Per row: top-k of x[r, 0:n] (values reduced by max over groups of `reduce_c` consecutive
+ * columns first when reduce_c > 1; sigmoid applied first when apply_sigmoid), sorted by
+ * value descending, ties by lower index. vals may be NULL. Requires k <= 512. */
+int sp_topk_rows(const float* x, int64_t ldx, int rows, int n, int reduce_c, int apply_sigmoid,
+                 int k, float* vals, int32_t* idx, void* stream);
+/* dst[b, i, :] = src[b*src_rows + idx[b, i], :] */
+int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,
+                   int batch, int d, float* dst, int64_t ld_dst, void* stream);
+/* ref[b,i,:] = sigmoid(delta[b,i,:] + anchors[idx[b,i],:]) (M2:1597-1603, M2:616). */
+int sp_ref_init(const float* delta, int64_t ld_delta, const float* anchors, const int32_t* idx,
+                int batch, int k, float* ref, void* stream);
+/* ref = sigmoid(delta + inverse_sigmoid(ref, 1e-5)) (M2:636-639, M2:548-552). */
+int sp_box_refine(const float* delta, int64_t ld_delta, float* ref, int rows, void* stream);
+/* post_process_object_detection, use_focal_loss=True (IPP:536-576):
+ * scores = sigmoid(logits) → top-k over Q*C → label = i % C, query = i / C, box = xyxy(boxes[query])
+ * × (w, h, w, h); counts[b] = #(score > threshold) (results are sorted, so the kept ones are a
+ * prefix). target_hw: device int32 [B, 2] (h, w). work: device int32 [B*k]. */
+int sp_postprocess(const float* logits, const float* boxes, const int32_t* target_hw, int batch,
+                   int q, int c, int k, float threshold, float* scores, int64_t* labels,
+                   float* boxes_xyxy, int32_t* counts, int32_t* work, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPOTTER_HIP_H */

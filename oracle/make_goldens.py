@@ -1,0 +1,132 @@
+"""TEST INFRASTRUCTURE ONLY — regenerate tests/golden/*.npz from the reference's HF path.
+
+Runs the reference's own call pattern (serve.py:98-109): HF
+`RTDetrImageProcessorPil` → `RTDetrV2ForObjectDetection` (built by
+oracle/hf_ref.py with spotter_amd.weights.generate(cfg, seed=0)) →
+`post_process_object_detection(threshold=0.5, target_sizes=[(h, w)])`, on
+seeded synthetic images (spotter_amd.synthetic) plus the reference's own test
+fixture image (apps/spotter/tests/spotter/test_data/test_pic.jpg, copied to
+tests/golden/test_pic.jpg as data). Only inputs' seeds, output tensors and
+digests are stored — no reference source.
+
+    python -m oracle.make_goldens            # all presets
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+PRE_SIZES = [(480, 800), (1280, 1280), (333, 517), (640, 640), (300, 200), (1080, 1920),
+             (717, 1200), (2160, 3840), (640, 1000), (700, 640), (1, 1), (2, 3000)]
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def load_test_pic():
+    from PIL import Image
+
+    with Image.open(os.path.join(GOLD, "test_pic.jpg")) as im:
+        return np.asarray(im.convert("RGB"))
+
+
+def make_preprocess():
+    from PIL import Image
+
+    from oracle.hf_ref import build_hf_processor
+    from spotter_amd.synthetic import synthetic_image
+
+    pp = build_hf_processor()
+    rec = {"sizes": [], "digests": [], "seeds": []}
+    for out_size in (640, 1280):
+        pp.size = {"height": out_size, "width": out_size}
+        for (h, w) in PRE_SIZES:
+            seed = h * 7 + w
+            img = synthetic_image(seed, h, w)
+            pv = pp(images=Image.fromarray(img), return_tensors="np")["pixel_values"][0]
+            rec["sizes"].append((h, w, out_size))
+            rec["seeds"].append(seed)
+            rec["digests"].append(sha(pv.astype(np.float32)))
+        img = load_test_pic()
+        pv = pp(images=Image.fromarray(img), return_tensors="np")["pixel_values"][0]
+        rec["sizes"].append((img.shape[0], img.shape[1], out_size))
+        rec["seeds"].append(-1)
+        rec["digests"].append(sha(pv.astype(np.float32)))
+    np.savez_compressed(os.path.join(GOLD, "preprocess.npz"), sizes=np.array(rec["sizes"]),
+                        seeds=np.array(rec["seeds"]), digests=np.array(rec["digests"]))
+
+
+def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=None):
+    import torch
+    from PIL import Image
+
+    from oracle.hf_ref import build_hf_model, build_hf_processor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.synthetic import synthetic_image
+    from spotter_amd.weights import generate
+
+    torch.manual_seed(0)
+    cfg = PRESETS[preset]
+    w = generate(cfg, seed=0)
+    model = build_hf_model(cfg, w)
+    pp = build_hf_processor()
+    pp.size = {"height": size, "width": size}
+    imgs = [synthetic_image(s, size, size) for s in seeds]
+    if with_pic:
+        imgs.append(load_test_pic())
+    out = {"seeds": np.array(list(seeds) + ([-1] if with_pic else [])), "size": size}
+    hooks = {}
+    model.model.enc_score_head.register_forward_hook(
+        lambda m, i, o: hooks.__setitem__("enc_cls", o.detach().numpy()))
+    logits, boxes, topk, encmax, dets = [], [], [], [], []
+    for img in imgs:
+        inputs = pp(images=Image.fromarray(img), return_tensors="pt")
+        with torch.no_grad():
+            o = model(**inputs)
+        ts = torch.tensor([[img.shape[0], img.shape[1]]])
+        r = pp.post_process_object_detection(o, target_sizes=ts, threshold=0.5)[0]
+        logits.append(o.logits[0].numpy())
+        boxes.append(o.pred_boxes[0].numpy())
+        ec = hooks["enc_cls"][0]
+        encmax.append(ec.max(-1))
+        _, ti = torch.topk(torch.from_numpy(ec).max(-1).values, cfg.num_queries)
+        topk.append(ti.numpy())
+        dets.append((r["scores"].numpy(), r["labels"].numpy(), r["boxes"].numpy(),
+                     np.array([img.shape[0], img.shape[1]])))
+    out["logits"] = np.stack(logits)
+    out["pred_boxes"] = np.stack(boxes)
+    out["enc_topk_ind"] = np.stack(topk)
+    out["enc_score_max"] = np.stack(encmax)
+    out["det_counts"] = np.array([len(d[0]) for d in dets])
+    out["det_scores"] = np.concatenate([d[0] for d in dets]) if dets else np.zeros(0)
+    out["det_labels"] = np.concatenate([d[1] for d in dets])
+    out["det_boxes"] = np.concatenate([d[2] for d in dets]).reshape(-1, 4)
+    out["target_sizes"] = np.stack([d[3] for d in dets])
+    name = tag or f"{preset}_{size}"
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **out)
+    print(name, "detections per image", out["det_counts"].tolist())
+
+
+def main(argv):
+    sys.path.insert(0, ROOT)
+    what = argv[1:] or ["preprocess", "r18vd", "r101vd"]
+    if "preprocess" in what:
+        make_preprocess()
+    if "r18vd" in what:
+        make_model("r18vd")
+    if "r101vd" in what:
+        make_model("r101vd")
+    if "r101vd_1280" in what:
+        make_model("r101vd", size=1280, seeds=(0,), with_pic=True, tag="r101vd_1280")
+
+
+if __name__ == "__main__":
+    main(sys.argv)

@@ -1,0 +1,99 @@
+"""Model hyper-parameters for the RT-DETRv2 presets the bench and tests use.
+
+Mirrors the fields of HF `RTDetrV2Config` (transformers/models/rt_detr_v2/
+configuration_rt_detr_v2.py:136-189) and `RTDetrResNetConfig`
+(transformers/models/rt_detr/configuration_rt_detr_resnet.py:58-67) that the
+inference path reads. Presets reproduce the published parameter counts
+(R101vd 76,556,268; R18vd 20,174,608 — SURVEY.md §6, §8 D1.2).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field
+
+# HF COCO label names in RT-DETR's contiguous 0..79 order (the names that
+# AMENITIES_MAPPING keys use, reference serve.py:31-59: "tv", "couch",
+# "dining table", "hair drier" …).
+COCO_NAMES = [
+    "person", "bicycle", "car", "motorcycle", "airplane", "bus", "train", "truck", "boat",
+    "traffic light", "fire hydrant", "stop sign", "parking meter", "bench", "bird", "cat",
+    "dog", "horse", "sheep", "cow", "elephant", "bear", "zebra", "giraffe", "backpack",
+    "umbrella", "handbag", "tie", "suitcase", "frisbee", "skis", "snowboard", "sports ball",
+    "kite", "baseball bat", "baseball glove", "skateboard", "surfboard", "tennis racket",
+    "bottle", "wine glass", "cup", "fork", "knife", "spoon", "bowl", "banana", "apple",
+    "sandwich", "orange", "broccoli", "carrot", "hot dog", "pizza", "donut", "cake", "chair",
+    "couch", "potted plant", "bed", "dining table", "toilet", "tv", "laptop", "mouse",
+    "remote", "keyboard", "cell phone", "microwave", "oven", "toaster", "sink",
+    "refrigerator", "book", "clock", "vase", "scissors", "teddy bear", "hair drier",
+    "toothbrush",
+]
+COCO_ID2LABEL = {i: n for i, n in enumerate(COCO_NAMES)}
+
+
+@dataclass
+class SpotterConfig:
+    name: str = "r101vd"
+    # backbone (RTDetrResNetConfig)
+    depths: list = field(default_factory=lambda: [3, 4, 23, 3])
+    hidden_sizes: list = field(default_factory=lambda: [256, 512, 1024, 2048])
+    layer_type: str = "bottleneck"
+    embedding_size: int = 64
+    # hybrid encoder
+    encoder_hidden_dim: int = 384
+    encoder_ffn_dim: int = 2048
+    encoder_attention_heads: int = 8
+    encoder_in_channels: list = field(default_factory=lambda: [512, 1024, 2048])
+    feat_strides: list = field(default_factory=lambda: [8, 16, 32])
+    hidden_expansion: float = 1.0
+    positional_encoding_temperature: float = 10000.0
+    # decoder
+    d_model: int = 256
+    decoder_in_channels: list = field(default_factory=lambda: [384, 384, 384])
+    decoder_ffn_dim: int = 1024
+    decoder_layers: int = 6
+    decoder_attention_heads: int = 8
+    decoder_n_levels: int = 3
+    decoder_n_points: int = 4
+    decoder_offset_scale: float = 0.5
+    num_queries: int = 300
+    num_labels: int = 80
+    layer_norm_eps: float = 1e-5
+    batch_norm_eps: float = 1e-5
+    image_size: int = 640
+    id2label: dict = field(default_factory=lambda: dict(COCO_ID2LABEL))
+
+    @property
+    def label2id(self):
+        return {v: k for k, v in self.id2label.items()}
+
+    def replace(self, **kw) -> "SpotterConfig":
+        return dataclasses.replace(self, **kw)
+
+    def to_hf_kwargs(self) -> dict:
+        """Keyword arguments for HF RTDetrV2Config / RTDetrResNetConfig (oracle side)."""
+        return dict(
+            backbone=dict(depths=list(self.depths), hidden_sizes=list(self.hidden_sizes),
+                          layer_type=self.layer_type, embedding_size=self.embedding_size,
+                          out_indices=[2, 3, 4]),
+            model=dict(encoder_hidden_dim=self.encoder_hidden_dim,
+                       encoder_ffn_dim=self.encoder_ffn_dim,
+                       encoder_in_channels=list(self.encoder_in_channels),
+                       decoder_in_channels=list(self.decoder_in_channels),
+                       hidden_expansion=self.hidden_expansion,
+                       decoder_layers=self.decoder_layers, d_model=self.d_model,
+                       decoder_ffn_dim=self.decoder_ffn_dim, num_queries=self.num_queries,
+                       num_labels=self.num_labels, id2label=dict(self.id2label)),
+        )
+
+    def to_json(self) -> str:
+        return json.dumps(dataclasses.asdict(self))
+
+
+R101VD = SpotterConfig()
+R18VD = SpotterConfig(
+    name="r18vd", depths=[2, 2, 2, 2], hidden_sizes=[64, 128, 256, 512], layer_type="basic",
+    encoder_hidden_dim=256, encoder_ffn_dim=1024, encoder_in_channels=[128, 256, 512],
+    decoder_in_channels=[256, 256, 256], decoder_layers=3, hidden_expansion=0.5,
+)
+PRESETS = {"r101vd": R101VD, "r18vd": R18VD}

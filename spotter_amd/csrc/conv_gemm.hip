@@ -1,0 +1,277 @@
+// Implicit-GEMM convolution / linear layer on fp32 MFMA (gfx950).
+//
+// One kernel covers every conv and nn.Linear on the RT-DETRv2 path: the
+// ResNet-vd backbone (RN:38-68, RN:179-231), encoder input projections
+// (M2:1350-1360), CCFM convs (M2:817-835, M2:907-952), AIFI / decoder
+// projections and FFNs (M2:228-242, M2:273-336), MSDA value/offset/weight/
+// output projections (M2:144-147) and the heads (M2:1376-1381, M2:1777-1787).
+//
+// Math: out[m, n] = epilogue(Σ_k A[m, k] · W[n, k]) with A gathered on the fly
+// from NHWC activations (im2col never materialised) and W stored [Cout][K]
+// (k contiguous). Tile BM×BN×32 per 256-thread workgroup (2×2 waves), each
+// wave a (32·TM)×(32·TN) patch of v_mfma_f32_32x32x2f32 accumulators (exact
+// fp32 fmaf chains, 64 FLOP/clk/SIMD). A and B tiles are staged through LDS as
+// row-major [row][32 k] with a 16-byte-chunk XOR swizzle so the per-lane
+// ds_read_b128 fragment reads are conflict-free; the k order inside an 8-deep
+// slab is permuted (lane half h owns k = 8s + 4h + j) identically for A and B,
+// which lets one ds_read_b128 feed four MFMAs. Global loads for tile t+1 are
+// issued before the MFMAs of tile t (register staging).
+//
+// Epilogue (fused): row mask (query-selection valid_mask, M2:1592), per-channel
+// BatchNorm scale/shift (FrozenBN M2:748-758 / eval BN), residual, activation,
+// post-activation residual, and a grouped output row map so projections write
+// straight into concatenated / flattened buffers (M2:1553-1555).
+#include "common.h"
+
+namespace sp {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int BK = 32;
+
+struct ConvArgs {
+  sp_conv_desc d;
+  int64_t M;
+  int32_t K;
+  int32_t HoWo;
+  int32_t fast;  // Cin % 32 == 0
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 2); }
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+  if (act == SP_ACT_RELU) return fmaxf(v, 0.0f);
+  if (act == SP_ACT_SILU) return v / (1.0f + expf(-v));
+  if (act == SP_ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+  return v;
+}
+
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
+  constexpr int BM = 64 * TM;
+  constexpr int BN = 64 * TN;
+  constexpr int PA = BM / 32;  // loader passes (32 rows per pass)
+  constexpr int PB = BN / 32;
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * BK];
+  float* As = smem;
+  float* Bs = smem + BM * BK;
+
+  const sp_conv_desc& d = p.d;
+  const int tid = threadIdx.x;
+  const int lrow = tid >> 3;   // 0..31
+  const int lchunk = tid & 7;  // 16-byte chunk of the 32-wide k slab
+  const int64_t m0 = (int64_t)blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN;
+
+  // Per-row implicit-im2col state for this thread's A rows (fixed across k).
+  int a_iy0[PA], a_ix0[PA], a_base[PA];
+  bool a_ok[PA];
+#pragma unroll
+  for (int i = 0; i < PA; ++i) {
+    int64_t m = m0 + i * 32 + lrow;
+    a_ok[i] = m < p.M;
+    int64_t mm = a_ok[i] ? m : 0;
+    int b = (int)(mm / p.HoWo);
+    int rem = (int)(mm - (int64_t)b * p.HoWo);
+    int oy = rem / d.Wo;
+    int ox = rem - oy * d.Wo;
+    a_iy0[i] = oy * d.stride - d.pad;
+    a_ix0[i] = ox * d.stride - d.pad;
+    a_base[i] = b * d.H;
+  }
+
+  float4 ra[PA], rb[PB];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    if (p.fast) {
+      const int tap = k0 / d.Cin;
+      const int c0 = k0 - tap * d.Cin + lchunk * 4;
+      const int kh = tap / d.KW;
+      const int kw = tap - kh * d.KW;
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        const int iy = a_iy0[i] + kh;
+        const int ix = a_ix0[i] + kw;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (a_ok[i] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W) {
+          const int64_t pix = (int64_t)(a_base[i] + iy) * d.W + ix;
+          v = *reinterpret_cast<const float4*>(d.A + pix * d.lda + c0);
+          if (d.A2) {
+            float4 w = *reinterpret_cast<const float4*>(d.A2 + pix * d.lda2 + c0);
+            v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+          }
+        }
+        ra[i] = v;
+      }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        const int n = n0 + i * 32 + lrow;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < d.Cout) v = *reinterpret_cast<const float4*>(d.Wt + (int64_t)n * p.K + k0 + lchunk * 4);
+        rb[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < PA; ++i) {
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + lchunk * 4 + j;
+          float v = 0.f;
+          if (a_ok[i] && k < p.K) {
+            const int tap = k / d.Cin;
+            const int c = k - tap * d.Cin;
+            const int kh = tap / d.KW;
+            const int kw = tap - kh * d.KW;
+            const int iy = a_iy0[i] + kh;
+            const int ix = a_ix0[i] + kw;
+            if ((unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W) {
+              const int64_t pix = (int64_t)(a_base[i] + iy) * d.W + ix;
+              v = d.A[pix * d.lda + c];
+              if (d.A2) v += d.A2[pix * d.lda2 + c];
+            }
+          }
+          e[j] = v;
+        }
+        ra[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        const int n = n0 + i * 32 + lrow;
+        float e[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + lchunk * 4 + j;
+          e[j] = (n < d.Cout && k < p.K) ? d.Wt[(int64_t)n * p.K + k] : 0.f;
+        }
+        rb[i] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  };
+
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  const int nk = (p.K + BK - 1) / BK;
+  load_tile(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PA; ++i)
+      *reinterpret_cast<float4*>(As + swz(i * 32 + lrow, lchunk)) = ra[i];
+#pragma unroll
+    for (int i = 0; i < PB; ++i)
+      *reinterpret_cast<float4*>(Bs + swz(i * 32 + lrow, lchunk)) = rb[i];
+    __syncthreads();
+    if (kt + 1 < nk) load_tile(kt + 1);
+#pragma unroll
+    for (int s = 0; s < BK / 8; ++s) {
+      float4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const float4*>(As + swz(wm * TM * 32 + i * 32 + r, s * 2 + h));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const float4*>(Bs + swz(wn * TN * 32 + j * 32 + r, s * 2 + h));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+  }
+
+  // Epilogue. acc[i][j][q] is (row (q&3) + 8*(q>>2) + 4*h, col r) of 32×32 subtile (i, j).
+  const int rpg = d.out_rows_per_group > 0 ? d.out_rows_per_group : 0x7fffffff;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * TN * 32 + j * 32 + r;
+    if (n >= d.Cout) continue;
+    const float sc = d.scale ? d.scale[n] : 1.0f;
+    const float sh = d.shift ? d.shift[n] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int64_t m = m0 + wm * TM * 32 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (m >= p.M) continue;
+        float v = acc[i][j][q];
+        if (d.row_scale) v *= d.row_scale[m % d.row_period];
+        v = fmaf(v, sc, sh);
+        if (d.res1) v += d.res1[m * d.ldr1 + n];
+        v = act_apply(v, d.act);
+        if (d.res2) v += d.res2[m * d.ldr2 + n];
+        const int64_t g = m / rpg;
+        const int64_t rr = m - g * rpg;
+        d.C[g * d.out_group_stride + rr * d.ldc + n] = v;
+      }
+    }
+  }
+}
+
+template <int TM, int TN>
+int launch(const ConvArgs& a, hipStream_t s) {
+  constexpr int BM = 64 * TM, BN = 64 * TN;
+  dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM));
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN>), grid, dim3(256), 0, s, a);
+  return check_launch("sp_conv2d");
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(d != nullptr, "sp_conv2d: null descriptor");
+  SP_ARG_CHECK(d->A && d->Wt && d->C, "sp_conv2d: null A/W/C");
+  SP_ARG_CHECK(d->N > 0 && d->H > 0 && d->W > 0 && d->Cin > 0 && d->Cout > 0,
+               "sp_conv2d: bad shape N=%d H=%d W=%d Cin=%d Cout=%d", d->N, d->H, d->W, d->Cin,
+               d->Cout);
+  SP_ARG_CHECK(d->KH > 0 && d->KW > 0 && d->stride > 0 && d->pad >= 0, "sp_conv2d: bad kernel");
+  const int ho = (d->H + 2 * d->pad - d->KH) / d->stride + 1;
+  const int wo = (d->W + 2 * d->pad - d->KW) / d->stride + 1;
+  SP_ARG_CHECK(ho == d->Ho && wo == d->Wo, "sp_conv2d: Ho/Wo %dx%d != expected %dx%d", d->Ho,
+               d->Wo, ho, wo);
+  SP_ARG_CHECK(d->lda >= d->Cin, "sp_conv2d: lda %lld < Cin %d", (long long)d->lda, d->Cin);
+  SP_ARG_CHECK(d->act >= 0 && d->act <= 3, "sp_conv2d: bad act %d", d->act);
+  SP_ARG_CHECK(!d->row_scale || d->row_period > 0, "sp_conv2d: row_period");
+  ConvArgs a;
+  a.d = *d;
+  a.M = (int64_t)d->N * ho * wo;
+  a.K = d->KH * d->KW * d->Cin;
+  a.HoWo = ho * wo;
+  a.fast = (d->Cin % BK == 0) ? 1 : 0;
+  if (a.fast) {
+    // float4 loads: 16-byte aligned rows and bases
+    const bool al = (d->lda % 4 == 0) && ((reinterpret_cast<uintptr_t>(d->A) & 15) == 0) &&
+                    ((reinterpret_cast<uintptr_t>(d->Wt) & 15) == 0) &&
+                    (!d->A2 || ((d->lda2 % 4 == 0) && ((reinterpret_cast<uintptr_t>(d->A2) & 15) == 0)));
+    if (!al) a.fast = 0;
+  }
+  hipStream_t s = as_stream(stream);
+  const int64_t mt128 = (a.M + 127) / 128;
+  const int nt128 = (d->Cout + 127) / 128;
+  const int nt64 = (d->Cout + 63) / 64;
+  if (d->Cout > 64 && mt128 * nt128 >= 480) return launch<2, 2>(a, s);
+  if (mt128 * nt64 >= 480) return launch<2, 1>(a, s);
+  return launch<1, 1>(a, s);
+}

@@ -1,0 +1,247 @@
+// Memory-bound helpers of the RT-DETRv2 path (NHWC, fp32, float4-vectorised).
+//   maxpool 3×3/2 (RN:88), avgpool 2×2 ceil (RN:150/202), nearest ×2 upsample
+//   into a concat slice (M2:1192-1193), LayerNorm (nn.LayerNorm), row gather
+//   (M2:1601-1617), reference-box init / refinement (M2:616, M2:636-639).
+#include "common.h"
+
+namespace sp {
+namespace {
+
+__device__ __forceinline__ int64_t grid_stride() { return (int64_t)gridDim.x * blockDim.x; }
+__device__ __forceinline__ int64_t gtid() { return (int64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+
+inline unsigned grid_for(int64_t work, int block = 256) {
+  int64_t g = (work + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// c4 = channels / 4
+__global__ void maxpool3s2_kernel(const float4* __restrict__ x, float4* __restrict__ y, int n, int h,
+                                  int w, int c4, int ho, int wo) {
+  const int64_t total = (int64_t)n * ho * wo * c4;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int cc = (int)(i % c4);
+    int64_t p = i / c4;
+    int ox = (int)(p % wo);
+    int64_t q = p / wo;
+    int oy = (int)(q % ho);
+    int b = (int)(q / ho);
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int dy = 0; dy < 3; ++dy) {
+      int iy = oy * 2 - 1 + dy;
+      if ((unsigned)iy >= (unsigned)h) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        int ix = ox * 2 - 1 + dx;
+        if ((unsigned)ix >= (unsigned)w) continue;
+        float4 v = x[(((int64_t)b * h + iy) * w + ix) * c4 + cc];
+        m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+      }
+    }
+    y[i] = m;
+  }
+}
+
+__global__ void avgpool2_kernel(const float4* __restrict__ x, float4* __restrict__ y, int n, int h,
+                                int w, int c4, int ho, int wo) {
+  const int64_t total = (int64_t)n * ho * wo * c4;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int cc = (int)(i % c4);
+    int64_t p = i / c4;
+    int ox = (int)(p % wo);
+    int64_t q = p / wo;
+    int oy = (int)(q % ho);
+    int b = (int)(q / ho);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int cnt = 0;
+    for (int dy = 0; dy < 2; ++dy) {
+      int iy = oy * 2 + dy;
+      if (iy >= h) continue;
+      for (int dx = 0; dx < 2; ++dx) {
+        int ix = ox * 2 + dx;
+        if (ix >= w) continue;
+        float4 v = x[(((int64_t)b * h + iy) * w + ix) * c4 + cc];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        ++cnt;
+      }
+    }
+    const float inv = (float)cnt;
+    y[i] = make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
+  }
+}
+
+__global__ void upsample2_kernel(const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+                                 int64_t ldy, int n, int h, int w, int c4) {
+  const int ho = 2 * h, wo = 2 * w;
+  const int64_t total = (int64_t)n * ho * wo * c4;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int cc = (int)(i % c4);
+    int64_t p = i / c4;
+    int ox = (int)(p % wo);
+    int64_t q = p / wo;
+    int oy = (int)(q % ho);
+    int b = (int)(q / ho);
+    const float4 v = *reinterpret_cast<const float4*>(x + (((int64_t)b * h + oy / 2) * w + ox / 2) * ldx + cc * 4);
+    *reinterpret_cast<float4*>(y + p * ldy + cc * 4) = v;
+  }
+}
+
+// One wave per row; d <= 1024 (16 floats per lane).
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t ldx,
+                                                         const float* __restrict__ g,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ y, int64_t ldy,
+                                                         int rows, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * ldx;
+  float v[16];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    int c = lane + 64 * i;
+    v[i] = c < d ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    int c = lane + 64 * i;
+    float t = c < d ? v[i] - mean : 0.f;
+    q += t * t;
+  }
+  const float var = wave_sum(q) / (float)d;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  float* yr = y + row * ldy;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    int c = lane + 64 * i;
+    if (c < d) yr[c] = (v[i] - mean) * rstd * g[c] + b[c];
+  }
+}
+
+__global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src, int src_rows,
+                                   const int32_t* __restrict__ idx, int k, int batch, int d,
+                                   float* __restrict__ dst, int64_t ld_dst) {
+  const int64_t total = (int64_t)batch * k * d;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int c = (int)(i % d);
+    int64_t r = i / d;  // b*k + j
+    int b = (int)(r / k);
+    int64_t s = (int64_t)b * src_rows + idx[r];
+    dst[r * ld_dst + c] = src[s * ld_src + c];
+  }
+}
+
+__global__ void ref_init_kernel(const float* __restrict__ delta, int64_t ld, const float* __restrict__ anchors,
+                                const int32_t* __restrict__ idx, int batch, int k,
+                                float* __restrict__ ref) {
+  const int64_t total = (int64_t)batch * k * 4;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int c = (int)(i & 3);
+    int64_t r = i >> 2;
+    float u = delta[r * ld + c] + anchors[(int64_t)idx[r] * 4 + c];
+    ref[i] = sigmoidf_(u);
+  }
+}
+
+__global__ void box_refine_kernel(const float* __restrict__ delta, int64_t ld, float* __restrict__ ref,
+                                  int rows) {
+  const int64_t total = (int64_t)rows * 4;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int c = (int)(i & 3);
+    int64_t r = i >> 2;
+    float x = fminf(fmaxf(ref[i], 0.f), 1.f);
+    float x1 = fmaxf(x, 1e-5f);
+    float x2 = fmaxf(1.f - x, 1e-5f);
+    float inv = logf(x1 / x2);
+    ref[i] = sigmoidf_(delta[r * ld + c] + inv);
+  }
+}
+
+// NCHW pixel_values (the processor contract, IPP:461-462) → NHWC for the stem conv.
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ x, float* __restrict__ y, int n, int c, int hw) {
+  const int64_t total = (int64_t)n * c * hw;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    int cc = (int)(i % c);
+    int64_t p = i / c;
+    int b = (int)(p / hw);
+    int s = (int)(p - (int64_t)b * hw);
+    y[i] = x[((int64_t)b * c + cc) * hw + s];
+  }
+}
+
+}  // namespace
+}  // namespace sp
+
+using namespace sp;
+
+extern "C" int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && c > 0 && h > 0 && w > 0, "sp_nchw_to_nhwc: bad args");
+  int64_t work = (int64_t)n * c * h * w;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x, y, n, c,
+                     h * w);
+  return check_launch("sp_nchw_to_nhwc");
+}
+
+extern "C" int sp_maxpool3x3s2(const float* x, float* y, int n, int h, int w, int c, void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "sp_maxpool3x3s2: bad args");
+  int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  int64_t work = (int64_t)n * ho * wo * (c / 4);
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo);
+  return check_launch("sp_maxpool3x3s2");
+}
+
+extern "C" int sp_avgpool2x2_ceil(const float* x, float* y, int n, int h, int w, int c, void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "sp_avgpool2x2_ceil: bad args");
+  int ho = (h + 1) / 2, wo = (w + 1) / 2;
+  int64_t work = (int64_t)n * ho * wo * (c / 4);
+  hipLaunchKernelGGL(avgpool2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo);
+  return check_launch("sp_avgpool2x2_ceil");
+}
+
+extern "C" int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, int n, int h,
+                                     int w, int c, void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && c % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0, "sp_upsample2x_nearest: bad args");
+  int64_t work = (int64_t)n * 4 * h * w * (c / 4);
+  hipLaunchKernelGGL(upsample2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x, ldx, y,
+                     ldy, n, h, w, c / 4);
+  return check_launch("sp_upsample2x_nearest");
+}
+
+extern "C" int sp_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float* y,
+                            int64_t ldy, int rows, int d, float eps, void* stream) {
+  SP_ARG_CHECK(x && gamma && beta && y && rows > 0 && d > 0 && d <= 1024, "sp_layernorm: bad args");
+  hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, ldx,
+                     gamma, beta, y, ldy, rows, d, eps);
+  return check_launch("sp_layernorm");
+}
+
+extern "C" int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,
+                              int batch, int d, float* dst, int64_t ld_dst, void* stream) {
+  SP_ARG_CHECK(src && idx && dst && k > 0 && batch > 0 && d > 0, "sp_gather_rows: bad args");
+  int64_t work = (int64_t)batch * k * d;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), src,
+                     ld_src, src_rows, idx, k, batch, d, dst, ld_dst);
+  return check_launch("sp_gather_rows");
+}
+
+extern "C" int sp_ref_init(const float* delta, int64_t ld_delta, const float* anchors, const int32_t* idx,
+                           int batch, int k, float* ref, void* stream) {
+  SP_ARG_CHECK(delta && anchors && idx && ref && batch > 0 && k > 0, "sp_ref_init: bad args");
+  hipLaunchKernelGGL(ref_init_kernel, dim3(grid_for((int64_t)batch * k * 4)), dim3(256), 0,
+                     as_stream(stream), delta, ld_delta, anchors, idx, batch, k, ref);
+  return check_launch("sp_ref_init");
+}
+
+extern "C" int sp_box_refine(const float* delta, int64_t ld_delta, float* ref, int rows, void* stream) {
+  SP_ARG_CHECK(delta && ref && rows > 0, "sp_box_refine: bad args");
+  hipLaunchKernelGGL(box_refine_kernel, dim3(grid_for((int64_t)rows * 4)), dim3(256), 0,
+                     as_stream(stream), delta, ld_delta, ref, rows);
+  return check_launch("sp_box_refine");
+}

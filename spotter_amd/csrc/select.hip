@@ -1,0 +1,193 @@
+// Per-row top-k by radix select (query selection and post-process).
+//
+// Query selection: torch.topk(enc_outputs_class.max(-1).values, 300) over the
+// 8,400 anchors at 640² (M2:1599). Post-process: torch.topk(sigmoid(logits)
+// .flatten(1), 300) over 300×80 (IPP:555-556), then label = i % C, query =
+// i // C, cxcywh→xyxy (IT:529-536) scaled by the original (w, h, w, h)
+// (IPP:538-549), keep score > threshold (IPP:572-574).
+//
+// One 1024-thread workgroup per row: keys (order-preserving uint32 of the
+// fp32 value, after the optional max-over-C reduction / sigmoid) live in LDS
+// (≤ 24,576 per row); four 8-bit radix passes find the k-th largest key T;
+// keys > T are compacted, keys == T are taken in index order; a bitonic sort on
+// (key desc, index asc) orders the k winners. Deterministic.
+#include "common.h"
+
+namespace sp {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kMaxN = 24576;
+constexpr int kMaxK = 512;
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+__global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict__ x, int64_t ldx, int n,
+                                                         int reduce_c, int apply_sigmoid, int k,
+                                                         float* __restrict__ vals,
+                                                         int32_t* __restrict__ idx_out) {
+  __shared__ uint32_t keys[kMaxN];
+  __shared__ uint32_t hist[256];
+  __shared__ unsigned long long cand[kMaxK];
+  __shared__ uint32_t s_sel[4];  // prefix, remaining, count_gt, count_eq
+  __shared__ uint32_t wave_tot[kThreads / 64];
+
+  const int tid = threadIdx.x;
+  const int64_t row = blockIdx.x;
+  const float* xr = x + row * ldx;
+  for (int i = tid; i < n; i += kThreads) {
+    float v;
+    if (reduce_c > 1) {
+      const float* p = xr + (int64_t)i * reduce_c;
+      v = p[0];
+      for (int c = 1; c < reduce_c; ++c) v = fmaxf(v, p[c]);
+    } else {
+      v = xr[i];
+    }
+    if (apply_sigmoid) v = sigmoidf_(v);
+    keys[i] = f2key(v);
+  }
+  for (int i = tid; i < kMaxK; i += kThreads) cand[i] = 0ull;
+  if (tid == 0) { s_sel[0] = 0; s_sel[1] = (uint32_t)k; s_sel[2] = 0; s_sel[3] = 0; }
+  __syncthreads();
+
+  uint32_t mask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kThreads) hist[i] = 0;
+    __syncthreads();
+    const uint32_t prefix = s_sel[0];
+    for (int i = tid; i < n; i += kThreads) {
+      const uint32_t key = keys[i];
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t rem = s_sel[1], cum = 0;
+      int bsel = 0;
+      for (int bin = 255; bin >= 0; --bin) {
+        if (cum + hist[bin] >= rem) { bsel = bin; break; }
+        cum += hist[bin];
+      }
+      s_sel[0] = prefix | ((uint32_t)bsel << shift);
+      s_sel[1] = rem - cum;
+    }
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  const uint32_t T = s_sel[0];
+  const uint32_t need_eq = s_sel[1];
+  const uint32_t n_gt = (uint32_t)k - need_eq;
+  // keys > T: any order (sorted below)
+  for (int i = tid; i < n; i += kThreads) {
+    const uint32_t key = keys[i];
+    if (key > T) {
+      uint32_t pos = atomicAdd(&s_sel[2], 1u);
+      cand[pos] = ((unsigned long long)key << 32) | (0xffffffffu - (uint32_t)i);
+    }
+  }
+  // keys == T: the first need_eq in index order (ordered block compaction)
+  const int lane = tid & 63, wid = tid >> 6;
+  uint32_t taken = 0;
+  for (int base = 0; base < n && taken < need_eq; base += kThreads) {
+    const int i = base + tid;
+    const bool f = i < n && keys[i] == T;
+    const unsigned long long bal = __ballot(f);
+    const uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_tot[wid] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+    for (int w = 0; w < kThreads / 64; ++w) {
+      if (w < wid) off += wave_tot[w];
+      tot += wave_tot[w];
+    }
+    const uint32_t pos = taken + off + before;
+    if (f && pos < need_eq)
+      cand[n_gt + pos] = ((unsigned long long)T << 32) | (0xffffffffu - (uint32_t)i);
+    taken += tot;
+    __syncthreads();
+  }
+  __syncthreads();
+  // bitonic sort of kMaxK entries, descending
+  for (int size = 2; size <= kMaxK; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < kMaxK / 2; t += kThreads) {
+        const int lo = 2 * stride * (t / stride) + (t % stride);
+        const int hi = lo + stride;
+        const bool desc = ((lo & size) == 0);
+        unsigned long long a = cand[lo], b = cand[hi];
+        if ((a < b) == desc) { cand[lo] = b; cand[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < k; i += kThreads) {
+    const unsigned long long e = cand[i];
+    const uint32_t key = (uint32_t)(e >> 32);
+    const uint32_t id = 0xffffffffu - (uint32_t)(e & 0xffffffffu);
+    idx_out[row * k + i] = (int32_t)id;
+    if (vals) vals[row * k + i] = key2f(key);
+  }
+}
+
+__global__ __launch_bounds__(512) void decode_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ target_hw,
+                                                     int q, int c, int k, float thr,
+                                                     const float* __restrict__ scores, const int32_t* __restrict__ idx,
+                                                     int64_t* __restrict__ labels, float* __restrict__ out_boxes,
+                                                     int32_t* __restrict__ counts) {
+  __shared__ int s_cnt;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const float ih = (float)target_hw[2 * b], iw = (float)target_hw[2 * b + 1];
+  for (int i = threadIdx.x; i < k; i += blockDim.x) {
+    const int32_t id = idx[(int64_t)b * k + i];
+    const int lab = id % c;
+    const int qq = id / c;
+    const float* bx = boxes + ((int64_t)b * q + qq) * 4;
+    const float cx = bx[0], cy = bx[1], w = bx[2], h = bx[3];
+    float* o = out_boxes + ((int64_t)b * k + i) * 4;
+    o[0] = (cx - 0.5f * w) * iw;
+    o[1] = (cy - 0.5f * h) * ih;
+    o[2] = (cx + 0.5f * w) * iw;
+    o[3] = (cy + 0.5f * h) * ih;
+    labels[(int64_t)b * k + i] = lab;
+    if (scores[(int64_t)b * k + i] > thr) atomicAdd(&s_cnt, 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) counts[b] = s_cnt;
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_topk_rows(const float* x, int64_t ldx, int rows, int n, int reduce_c, int apply_sigmoid,
+                            int k, float* vals, int32_t* idx, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(x && idx && rows > 0 && n > 0, "sp_topk_rows: bad args");
+  SP_ARG_CHECK(n <= kMaxN, "sp_topk_rows: n=%d > %d", n, kMaxN);
+  SP_ARG_CHECK(k > 0 && k <= kMaxK && k <= n, "sp_topk_rows: k=%d (n=%d, max %d)", k, n, kMaxK);
+  SP_ARG_CHECK(reduce_c >= 1, "sp_topk_rows: reduce_c");
+  hipLaunchKernelGGL(topk_kernel, dim3(rows), dim3(kThreads), 0, as_stream(stream), x, ldx, n, reduce_c,
+                     apply_sigmoid, k, vals, idx);
+  return check_launch("sp_topk_rows");
+}
+
+extern "C" int sp_postprocess(const float* logits, const float* boxes, const int32_t* target_hw, int batch,
+                              int q, int c, int k, float threshold, float* scores, int64_t* labels,
+                              float* boxes_xyxy, int32_t* counts, int32_t* work, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(logits && boxes && target_hw && scores && labels && boxes_xyxy && counts && work,
+               "sp_postprocess: null args");
+  int rc = sp_topk_rows(logits, (int64_t)q * c, batch, q * c, 1, 1, k, scores, work, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(decode_kernel, dim3(batch), dim3(512), 0, as_stream(stream), boxes, target_hw, q, c, k,
+                     threshold, scores, work, labels, boxes_xyxy, counts);
+  return check_launch("sp_postprocess");
+}

@@ -1,0 +1,476 @@
+"""The RT-DETRv2 forward on MI355X: weight packing + launch orchestration.
+
+Data layout in HBM (all fp32): activations NHWC (`[B, H, W, C]` = `[B·H·W, C]`
+rows), conv weights `[Cout][KH][KW][Cin]`, linear weights `[N][K]` (PyTorch's
+own), BatchNorm folded to per-channel (scale, shift) applied in the GEMM
+epilogue. Buffers are allocated once per (batch, size) and reused, so a
+forward allocates nothing (hipGraph-capturable). Fusions relative to the HF
+graph (transformers/models/rt_detr_v2/modeling_rt_detr_v2.py = M2,
+models/rt_detr/modeling_rt_detr_resnet.py = RN):
+
+* conv + BN + activation + residual in one GEMM epilogue (RN:225-231, M2:921-923)
+* CSPRep conv1 ‖ conv2 as one GEMM (same input, M2:949-951); the CSP sum
+  h1 + h2 as the last RepVGG block's post-activation residual (M2:952)
+* encoder_input_proj / lateral / downsample convs write straight into the
+  concat buffers (M2:1193, M2:1205); decoder_input_proj writes straight into
+  source_flatten (M2:1553-1555) through the grouped output row map
+* query selection's valid-mask multiply as a GEMM row scale (M2:1592)
+* q_proj ‖ k_proj as one GEMM with the +pos addend fused in the A loader
+  (M2:313-317); sampling_offsets ‖ attention_weights as one GEMM (M2:196-203)
+* all six decoder value_proj GEMMs as one N = 6·256 GEMM over source_flatten
+* enc_bbox_head evaluated only on the 300 selected rows (its other rows are
+  never read, M2:1601-1603) and class_embed only for the last decoder layer
+  (the only logits the output uses, M2:1880); both are dead-code elimination
+  with identical per-row math.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .config import SpotterConfig
+from .ops import V, view
+from .weights import backbone_plan
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
+
+
+class ConvW:
+    __slots__ = ("w", "cin", "cout", "k", "scale", "shift")
+
+    def __init__(self, w, cin, cout, k, scale, shift):
+        self.w, self.cin, self.cout, self.k, self.scale, self.shift = w, cin, cout, k, scale, shift
+
+
+class LinW:
+    __slots__ = ("w", "b", "k", "n")
+
+    def __init__(self, w, b, k, n):
+        self.w, self.b, self.k, self.n = w, b, k, n
+
+
+def frozen_bn_affine(p, pre):
+    # RTDetrV2FrozenBatchNorm2d.forward M2:751-757
+    scale = p[pre + ".weight"] * (p[pre + ".running_var"] + np.float32(1e-5)) ** np.float32(-0.5)
+    shift = p[pre + ".bias"] - p[pre + ".running_mean"] * scale
+    return scale.astype(np.float32), shift.astype(np.float32)
+
+
+def eval_bn_affine(p, pre, eps=1e-5):
+    # nn.BatchNorm2d eval: (x - mean) / sqrt(var + eps) * w + b
+    inv = (p[pre + ".running_var"] + np.float32(eps)) ** np.float32(-0.5)
+    scale = p[pre + ".weight"] * inv
+    shift = p[pre + ".bias"] - p[pre + ".running_mean"] * scale
+    return scale.astype(np.float32), shift.astype(np.float32)
+
+
+def conv_khwc(w):
+    co, ci, k, _ = w.shape
+    return np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(co, k * k * ci))
+
+
+def sine_pos_embed(h, w, dim, temperature):
+    """build_2d_sinusoidal_position_embedding M2:955-1000 (f64 on host, cast to f32; constant)."""
+    pd = dim // 4
+    omega = 1.0 / temperature ** (np.arange(pd, dtype=np.float64) / pd)
+    gh, gw = np.meshgrid(np.arange(h, dtype=np.float64), np.arange(w, dtype=np.float64), indexing="ij")
+    eh = np.outer(gh.reshape(-1), omega)
+    ew = np.outer(gw.reshape(-1), omega)
+    return np.concatenate([np.sin(eh), np.cos(eh), np.sin(ew), np.cos(ew)], 1).astype(np.float32)
+
+
+def anchors_for(shapes, grid_size=0.05):
+    """_cached_generate_anchors M2:1421-1449 (constant table, built once per shape set)."""
+    out = []
+    f = np.float32
+    for lvl, (h, w) in enumerate(shapes):
+        gy, gx = np.meshgrid(np.arange(h, dtype=f), np.arange(w, dtype=f), indexing="ij")
+        xy = np.stack([gx, gy], -1) + f(0.5)
+        xy[..., 0] /= f(w)
+        xy[..., 1] /= f(h)
+        wh = np.ones_like(xy) * f(grid_size * 2.0 ** lvl)
+        out.append(np.concatenate([xy, wh], -1).reshape(h * w, 4))
+    a = np.concatenate(out, 0).astype(f)
+    valid = ((a > f(1e-2)) & (a < f(1 - 1e-2))).all(-1)
+    lg = np.log(a / (f(1) - a)).astype(f)
+    lg[~valid] = np.finfo(f).max
+    return lg, valid.astype(f)
+
+
+class Engine:
+    """Owns the packed device weights and the per-shape workspaces of one GPU."""
+
+    def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda"):
+        from ._lib import lib
+
+        self.cfg = cfg
+        self.dev = torch.device(device)
+        if self.dev.type != "cuda":
+            raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
+        idx = self.dev.index if self.dev.index is not None else torch.cuda.current_device()
+        self.dev = torch.device("cuda", idx)
+        rc = lib().sp_device_init(idx)
+        if rc != 0:
+            raise RuntimeError(f"sp_device_init: {lib().sp_last_error().decode()}")
+        with torch.cuda.device(self.dev):
+            self._pack(weights)
+        self._ws = {}
+        self._consts = {}
+
+    # ------------------------------------------------------------------ weights
+    def _conv(self, p, conv_key, bn_pre, frozen):
+        w = p[conv_key]
+        co, ci, k, _ = w.shape
+        sc, sh = (frozen_bn_affine if frozen else eval_bn_affine)(p, bn_pre)
+        return ConvW(_t(conv_khwc(w), self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev))
+
+    def _lin(self, p, pre, *more):
+        ws = [p[pre + ".weight"]] + [p[m + ".weight"] for m in more]
+        bs = [p[pre + ".bias"]] + [p[m + ".bias"] for m in more]
+        w = np.concatenate(ws, 0)
+        b = np.concatenate(bs, 0)
+        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0])
+
+    def _ln(self, p, pre):
+        return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
+
+    def _pack(self, p):
+        cfg = self.cfg
+        bb = "model.backbone.model"
+        self.stem = [self._conv(p, f"{bb}.embedder.embedder.{i}.convolution.weight",
+                                f"{bb}.embedder.embedder.{i}.normalization", True) for i in range(3)]
+        self.blocks = []
+        for (s, i, lt, cin, cout, st, sc) in backbone_plan(cfg):
+            pre = f"{bb}.encoder.stages.{s}.layers.{i}"
+            blk = {"s": s, "i": i, "type": lt, "cin": cin, "cout": cout, "stride": st, "sc": sc}
+            if sc == "conv":
+                blk["short"] = self._conv(p, pre + ".shortcut.convolution.weight", pre + ".shortcut.normalization", True)
+            elif sc == "avgconv":
+                blk["short"] = self._conv(p, pre + ".shortcut.1.convolution.weight", pre + ".shortcut.1.normalization", True)
+            nl = 3 if lt == "bottleneck" else 2
+            blk["layers"] = [self._conv(p, f"{pre}.layer.{j}.convolution.weight", f"{pre}.layer.{j}.normalization", True)
+                             for j in range(nl)]
+            self.blocks.append(blk)
+        self.in_proj = [self._conv(p, f"model.encoder_input_proj.{l}.0.weight", f"model.encoder_input_proj.{l}.1", False)
+                        for l in range(len(cfg.encoder_in_channels))]
+        a = "model.encoder.aifi.0.layers.0"
+        self.aifi = {
+            "qk": self._lin(p, a + ".self_attn.q_proj", a + ".self_attn.k_proj"),
+            "v": self._lin(p, a + ".self_attn.v_proj"),
+            "o": self._lin(p, a + ".self_attn.o_proj"),
+            "ln1": self._ln(p, a + ".self_attn_layer_norm"),
+            "fc1": self._lin(p, a + ".mlp.fc1"),
+            "fc2": self._lin(p, a + ".mlp.fc2"),
+            "ln2": self._ln(p, a + ".final_layer_norm"),
+        }
+        E = "model.encoder"
+        nl = len(cfg.encoder_in_channels)
+        self.lateral = [self._conv(p, f"{E}.lateral_convs.{i}.conv.weight", f"{E}.lateral_convs.{i}.norm", False)
+                        for i in range(nl - 1)]
+        self.down = [self._conv(p, f"{E}.downsample_convs.{i}.conv.weight", f"{E}.downsample_convs.{i}.norm", False)
+                     for i in range(nl - 1)]
+        self.fpn = [self._csp(p, f"{E}.fpn_blocks.{i}") for i in range(nl - 1)]
+        self.pan = [self._csp(p, f"{E}.pan_blocks.{i}") for i in range(nl - 1)]
+        self.dec_proj = [self._conv(p, f"model.decoder_input_proj.{l}.0.weight", f"model.decoder_input_proj.{l}.1", False)
+                         for l in range(len(cfg.decoder_in_channels))]
+        self.enc_output = self._lin(p, "model.enc_output.0")
+        self.enc_ln = self._ln(p, "model.enc_output.1")
+        self.enc_score = self._lin(p, "model.enc_score_head")
+        self.enc_bbox = [self._lin(p, f"model.enc_bbox_head.layers.{i}") for i in range(3)]
+        self.qpos = [self._lin(p, f"model.decoder.query_pos_head.layers.{i}") for i in range(2)]
+        D = "model.decoder.layers"
+        L = cfg.decoder_layers
+        self.value_all = self._lin(p, f"{D}.0.encoder_attn.value_proj",
+                                   *[f"{D}.{j}.encoder_attn.value_proj" for j in range(1, L)])
+        self.dec = []
+        for j in range(L):
+            q = f"{D}.{j}"
+            self.dec.append({
+                "qk": self._lin(p, q + ".self_attn.q_proj", q + ".self_attn.k_proj"),
+                "v": self._lin(p, q + ".self_attn.v_proj"),
+                "o": self._lin(p, q + ".self_attn.o_proj"),
+                "ln1": self._ln(p, q + ".self_attn_layer_norm"),
+                "offaw": self._lin(p, q + ".encoder_attn.sampling_offsets", q + ".encoder_attn.attention_weights"),
+                "out": self._lin(p, q + ".encoder_attn.output_proj"),
+                "ln2": self._ln(p, q + ".encoder_attn_layer_norm"),
+                "fc1": self._lin(p, q + ".mlp.fc1"),
+                "fc2": self._lin(p, q + ".mlp.fc2"),
+                "ln3": self._ln(p, q + ".final_layer_norm"),
+                "bbox": [self._lin(p, f"model.decoder.bbox_embed.{j}.layers.{i}") for i in range(3)],
+            })
+        self.cls_last = self._lin(p, f"model.decoder.class_embed.{L - 1}")
+
+    def _csp(self, p, pre):
+        c1 = self._conv(p, pre + ".conv1.conv.weight", pre + ".conv1.norm", False)
+        c2 = self._conv(p, pre + ".conv2.conv.weight", pre + ".conv2.norm", False)
+        c12 = ConvW(torch.cat([c1.w, c2.w], 0).contiguous(), c1.cin, c1.cout + c2.cout, 1,
+                    torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous())
+        reps = [(self._conv(p, f"{pre}.bottlenecks.{b}.conv1.conv.weight", f"{pre}.bottlenecks.{b}.conv1.norm", False),
+                 self._conv(p, f"{pre}.bottlenecks.{b}.conv2.conv.weight", f"{pre}.bottlenecks.{b}.conv2.norm", False))
+                for b in range(3)]
+        c3 = None
+        if (pre + ".conv3.conv.weight") in p:
+            c3 = self._conv(p, pre + ".conv3.conv.weight", pre + ".conv3.norm", False)
+        return {"c12": c12, "hid": c1.cout, "reps": reps, "c3": c3}
+
+    # ------------------------------------------------------------------ workspace
+    def _buf(self, key, *shape, dtype=torch.float32):
+        ws = self._ws
+        t = ws.get(key)
+        n = int(np.prod(shape))
+        if t is None or t.numel() < n or t.dtype != dtype:
+            t = torch.empty(n, dtype=dtype, device=self.dev)
+            ws[key] = t
+        return t[:n]
+
+    def _const(self, key, fn):
+        c = self._consts.get(key)
+        if c is None:
+            c = fn()
+            self._consts[key] = c
+        return c
+
+    # ------------------------------------------------------------------ layers
+    def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
+        pad = cw.k // 2
+        return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
+                          shift=cw.shift, act=act, res1=res1, res2=res2, **kw)
+
+    def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None):
+        return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
+                          row_scale=row_scale)
+
+    def backbone(self, px_nhwc: torch.Tensor, B, H, W):
+        """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC)."""
+        e = self.cfg.embedding_size
+        h1, w1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        s0 = self._buf("stem0", B, h1, w1, e // 2)
+        s1 = self._buf("stem1", B, h1, w1, e // 2)
+        s2 = self._buf("stem2", B, h1, w1, e)
+        self._cv(view(px_nhwc, 3), B, H, W, self.stem[0], 2, view(s0, e // 2), act="relu")
+        self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act="relu")
+        self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act="relu")
+        h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
+        cur = self._buf("pool", B, h, w, e)
+        ops.maxpool3x3s2(s2, cur, B, h1, w1, e)
+        c = e
+        feats = []
+        nstage = len(self.cfg.depths)
+        for blk in self.blocks:
+            s, i, st, cout = blk["s"], blk["i"], blk["stride"], blk["cout"]
+            if i == 0 and s > 0:
+                feats.append((cur, h, w, c))
+            ho, wo = (h - 1) // st + 1, (w - 1) // st + 1
+            # shortcut (RN:199-207)
+            if blk["sc"] == "identity":
+                res = view(cur, c)
+            else:
+                src, sh_, sw_ = cur, h, w
+                if blk["sc"] == "avgconv":
+                    pooled = self._buf(f"s{s}_pool", B, (h + 1) // 2, (w + 1) // 2, c)
+                    ops.avgpool2x2_ceil(cur, pooled, B, h, w, c)
+                    src, sh_, sw_ = pooled, (h + 1) // 2, (w + 1) // 2
+                sbuf = self._buf(f"s{s}_sc", B, ho, wo, cout)
+                self._cv(view(src, c), B, sh_, sw_, blk["short"], 1 if blk["sc"] == "avgconv" else st, view(sbuf, cout))
+                res = view(sbuf, cout)
+            out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
+            L = blk["layers"]
+            if blk["type"] == "bottleneck":
+                red = L[0].cout
+                t1 = self._buf(f"s{s}_t1", B, h, w, red)
+                t2 = self._buf(f"s{s}_t2", B, ho, wo, red)
+                self._cv(view(cur, c), B, h, w, L[0], 1, view(t1, red), act="relu")
+                self._cv(view(t1, red), B, h, w, L[1], st, view(t2, red), act="relu")
+                self._cv(view(t2, red), B, ho, wo, L[2], 1, view(out, cout), act="relu", res1=res)
+            else:
+                t1 = self._buf(f"s{s}_t1", B, ho, wo, cout)
+                self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act="relu")
+                self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act="relu", res1=res)
+            cur, h, w, c = out, ho, wo, cout
+        feats.append((cur, h, w, c))
+        return feats[-3:] if nstage >= 3 else feats
+
+    def _csp_fwd(self, cs, x: V, B, h, w, out: V, tag):
+        """RTDetrV2CSPRepLayer.forward M2:948-952 on a 2·H-channel NHWC input."""
+        hid = cs["hid"]
+        c12 = self._buf(f"{tag}_c12", B, h, w, 2 * hid)
+        self._cv(x, B, h, w, cs["c12"], 1, view(c12, 2 * hid), act="silu")
+        h2 = V(c12, hid, 2 * hid)
+        cur = V(c12, 0, 2 * hid)
+        t = self._buf(f"{tag}_t", B, h, w, hid)
+        final_to_out = cs["c3"] is None
+        for b, (k3, k1) in enumerate(cs["reps"]):
+            last = b == len(cs["reps"]) - 1
+            self._cv(cur, B, h, w, k3, 1, view(t, hid))
+            if last and final_to_out:
+                dst = out
+            else:
+                dst = view(self._buf(f"{tag}_r{b % 2}", B, h, w, hid), hid)
+            self._cv(cur, B, h, w, k1, 1, dst, act="silu", res1=view(t, hid), res2=h2 if last else None)
+            cur = dst
+        if cs["c3"] is not None:
+            self._cv(cur, B, h, w, cs["c3"], 1, out, act="silu")
+
+    def encoder(self, feats, B):
+        """encoder_input_proj (M2:1512) + RTDetrV2HybridEncoder.forward (M2:1164-1209)."""
+        cfg = self.cfg
+        Hd = cfg.encoder_hidden_dim
+        (f0, h0, w0, c0), (f1, h1, w1, c1), (f2, h2, w2, c2) = feats
+        cat3 = self._buf("cat3", B, h0, w0, 2 * Hd)   # [up(lat1) | proj0]
+        cat4 = self._buf("cat4", B, h1, w1, 2 * Hd)   # [up(lat0) | proj1]
+        catn4 = self._buf("catn4", B, h1, w1, 2 * Hd)  # [down0 | lat1]
+        catn5 = self._buf("catn5", B, h2, w2, 2 * Hd)  # [down1 | lat0]
+        p5 = self._buf("p5", B, h2, w2, Hd)
+        self._cv(view(f0, c0), B, h0, w0, self.in_proj[0], 1, V(cat3, Hd, 2 * Hd))
+        self._cv(view(f1, c1), B, h1, w1, self.in_proj[1], 1, V(cat4, Hd, 2 * Hd))
+        self._cv(view(f2, c2), B, h2, w2, self.in_proj[2], 1, view(p5, Hd))
+        # AIFI on level 2 (M2:1058-1095; encoder layer M2:856-904, post-norm)
+        n = h2 * w2
+        rows = B * n
+        A = self.aifi
+        pos = self._const(("pos", B, h2, w2), lambda: _t(np.tile(
+            sine_pos_embed(h2, w2, Hd, cfg.positional_encoding_temperature), (B, 1)), self.dev))
+        qk = self._buf("aifi_qk", rows, 2 * Hd)
+        vv = self._buf("aifi_v", rows, Hd)
+        at = self._buf("aifi_at", rows, Hd)
+        t1 = self._buf("aifi_t1", rows, Hd)
+        y1 = self._buf("aifi_y1", rows, Hd)
+        ff = self._buf("aifi_ff", rows, cfg.encoder_ffn_dim)
+        t2 = self._buf("aifi_t2", rows, Hd)
+        p5a = self._buf("p5a", rows, Hd)
+        self._lin_op(view(p5, Hd), rows, A["qk"], view(qk, 2 * Hd), a2=view(pos, Hd))
+        self._lin_op(view(p5, Hd), rows, A["v"], view(vv, Hd))
+        heads = cfg.encoder_attention_heads
+        ops.attention(V(qk, 0, 2 * Hd), V(qk, Hd, 2 * Hd), view(vv, Hd), view(at, Hd), B, n, heads, Hd // heads,
+                      (Hd // heads) ** -0.5)
+        self._lin_op(view(at, Hd), rows, A["o"], view(t1, Hd), res1=view(p5, Hd))
+        ops.layernorm(view(t1, Hd), *A["ln1"], view(y1, Hd), rows, Hd, cfg.layer_norm_eps)
+        self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act="gelu")
+        self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(t2, Hd), res1=view(y1, Hd))
+        ops.layernorm(view(t2, Hd), *A["ln2"], view(p5a, Hd), rows, Hd, cfg.layer_norm_eps)
+        # FPN (M2:1183-1197)
+        self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act="silu")
+        ops.upsample2x(V(catn5, Hd, 2 * Hd), V(cat4, 0, 2 * Hd), B, h2, w2, Hd)
+        F4 = self._buf("F4", B, h1, w1, Hd)
+        self._csp_fwd(self.fpn[0], view(cat4, 2 * Hd), B, h1, w1, view(F4, Hd), "fpn0")
+        self._cv(view(F4, Hd), B, h1, w1, self.lateral[1], 1, V(catn4, Hd, 2 * Hd), act="silu")
+        ops.upsample2x(V(catn4, Hd, 2 * Hd), V(cat3, 0, 2 * Hd), B, h1, w1, Hd)
+        F3 = self._buf("F3", B, h0, w0, Hd)
+        self._csp_fwd(self.fpn[1], view(cat3, 2 * Hd), B, h0, w0, view(F3, Hd), "fpn1")
+        # PAN (M2:1199-1207)
+        self._cv(view(F3, Hd), B, h0, w0, self.down[0], 2, V(catn4, 0, 2 * Hd), act="silu")
+        N4 = self._buf("N4", B, h1, w1, Hd)
+        self._csp_fwd(self.pan[0], view(catn4, 2 * Hd), B, h1, w1, view(N4, Hd), "pan0")
+        self._cv(view(N4, Hd), B, h1, w1, self.down[1], 2, V(catn5, 0, 2 * Hd), act="silu")
+        N5 = self._buf("N5", B, h2, w2, Hd)
+        self._csp_fwd(self.pan[1], view(catn5, 2 * Hd), B, h2, w2, view(N5, Hd), "pan1")
+        return [(F3, h0, w0), (N4, h1, w1), (N5, h2, w2)]
+
+    def decoder_inputs(self, enc, B):
+        """decoder_input_proj + flatten/concat (M2:1533-1556) → source_flatten [B, S, d]."""
+        D = self.cfg.d_model
+        shapes = [(h, w) for (_, h, w) in enc]
+        S = sum(h * w for h, w in shapes)
+        starts = [0]
+        for h, w in shapes[:-1]:
+            starts.append(starts[-1] + h * w)
+        src = self._buf("src_flat", B, S, D)
+        Hd = self.cfg.encoder_hidden_dim
+        for l, (t, h, w) in enumerate(enc):
+            self._cv(view(t, Hd), B, h, w, self.dec_proj[l], 1, V(src, starts[l] * D, D),
+                     rows_per_group=h * w, group_stride=S * D)
+        return src, shapes, starts, S
+
+    def forward(self, pixel_values: torch.Tensor):
+        """pixel_values [B,3,H,W] fp32 (device) → (logits [B,Q,C], pred_boxes [B,Q,4]) (M2:1864-1881)."""
+        cfg = self.cfg
+        if pixel_values.device != self.dev:
+            pixel_values = pixel_values.to(self.dev, non_blocking=True)
+        pixel_values = pixel_values.contiguous()
+        if pixel_values.dtype != torch.float32:
+            raise TypeError("pixel_values must be float32")
+        B, C, H, W = pixel_values.shape
+        if C != 3:
+            raise ValueError("Make sure that the channel dimension of the pixel values match with the one set in the configuration.")
+        with torch.cuda.device(self.dev):
+            px = self._buf("px_nhwc", B, H, W, 3)
+            ops.nchw_to_nhwc(pixel_values, px)
+            feats = self.backbone(px, B, H, W)
+            enc = self.encoder(feats, B)
+            src, shapes, starts, S = self.decoder_inputs(enc, B)
+            return self.decode(src, shapes, starts, S, B)
+
+    def decode(self, src, shapes, starts, S, B):
+        cfg = self.cfg
+        D, Q, NC = cfg.d_model, cfg.num_queries, cfg.num_labels
+        # query selection (M2:1582-1623)
+        anchors, valid = self._const(("anchors", tuple(shapes)), lambda: tuple(
+            _t(a, self.dev) for a in anchors_for(shapes)))
+        rows = B * S
+        om_pre = self._buf("om_pre", rows, D)
+        om = self._buf("om", rows, D)
+        cls = self._buf("enc_cls", rows, NC)
+        self._lin_op(view(src, D), rows, self.enc_output, view(om_pre, D), row_scale=valid)
+        ops.layernorm(view(om_pre, D), *self.enc_ln, view(om, D), rows, D, cfg.layer_norm_eps)
+        self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
+        topk = self._buf("topk", B, Q, dtype=torch.int32)
+        ops.topk_rows(V(cls, 0, S * NC), B, S, Q, topk, reduce_c=NC)
+        Bq = B * Q
+        h = self._buf("dec_h", Bq, D)
+        ops.gather_rows(view(om, D), S, topk, Q, B, D, view(h, D))
+        t_a = self._buf("dec_ta", Bq, D)
+        t_b = self._buf("dec_tb", Bq, D)
+        delta = self._buf("dec_delta", Bq, 4)
+        self._lin_op(view(h, D), Bq, self.enc_bbox[0], view(t_a, D), act="relu")
+        self._lin_op(view(t_a, D), Bq, self.enc_bbox[1], view(t_b, D), act="relu")
+        self._lin_op(view(t_b, D), Bq, self.enc_bbox[2], view(delta, 4))
+        ref = self._buf("dec_ref", Bq, 4)
+        ops.ref_init(view(delta, 4), anchors, topk, B, Q, ref)
+        # all six value projections at once (M2:190)
+        L = cfg.decoder_layers
+        vall = self._buf("value_all", rows, L * D)
+        self._lin_op(view(src, D), rows, self.value_all, view(vall, L * D))
+        # decoder (M2:578-661)
+        nH, nL, nP = cfg.decoder_attention_heads, cfg.decoder_n_levels, cfg.decoder_n_points
+        qp = self._buf("dec_qp", Bq, 2 * D)
+        pos = self._buf("dec_pos", Bq, D)
+        qk = self._buf("dec_qk", Bq, 2 * D)
+        vv = self._buf("dec_v", Bq, D)
+        at = self._buf("dec_at", Bq, D)
+        tmp = self._buf("dec_tmp", Bq, D)
+        offaw = self._buf("dec_offaw", Bq, nH * nL * nP * 3)
+        ff = self._buf("dec_ff", Bq, cfg.decoder_ffn_dim)
+        logits = self._buf("logits", B, Q, NC)
+        for j, P in enumerate(self.dec):
+            self._lin_op(view(ref, 4), Bq, self.qpos[0], view(qp, 2 * D), act="relu")
+            self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
+            # self-attention, q = k = h + pos, v = h (M2:395-404)
+            self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
+            self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
+            ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
+                          (D // nH) ** -0.5)
+            self._lin_op(view(at, D), Bq, P["o"], view(tmp, D), res1=view(h, D))
+            ops.layernorm(view(tmp, D), *P["ln1"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            # deformable cross-attention (M2:409-423)
+            self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
+            ops.msda(V(vall, 0, L * D), j * D, view(offaw, nH * nL * nP * 3), ref, view(at, D), B, S, Q, nH,
+                     D // nH, shapes, starts, nP, cfg.decoder_offset_scale)
+            self._lin_op(view(at, D), Bq, P["out"], view(tmp, D), res1=view(h, D))
+            ops.layernorm(view(tmp, D), *P["ln2"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            # FFN (M2:426-429)
+            self._lin_op(view(h, D), Bq, P["fc1"], view(ff, cfg.decoder_ffn_dim), act="relu")
+            self._lin_op(view(ff, cfg.decoder_ffn_dim), Bq, P["fc2"], view(tmp, D), res1=view(h, D))
+            ops.layernorm(view(tmp, D), *P["ln3"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            # iterative box refinement (M2:636-639)
+            b0, b1, b2 = P["bbox"]
+            self._lin_op(view(h, D), Bq, b0, view(t_a, D), act="relu")
+            self._lin_op(view(t_a, D), Bq, b1, view(t_b, D), act="relu")
+            self._lin_op(view(t_b, D), Bq, b2, view(delta, 4))
+            ops.box_refine(view(delta, 4), ref, Bq)
+        self._lin_op(view(h, D), Bq, self.cls_last, view(logits, NC))
+        return logits.view(B, Q, NC), ref.view(B, Q, 4)

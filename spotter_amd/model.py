@@ -1,0 +1,121 @@
+"""SpotterForObjectDetection — drop-in for HF RTDetrV2ForObjectDetection on MI355X.
+
+The interface AmenitiesDetector relies on (reference serve.py:99-100, 111-114,
+199-205): ``model(**inputs)`` (under ``torch.no_grad()``) returning an object
+with ``.logits [B,300,80]`` and ``.pred_boxes [B,300,4]``; ``model.config.id2label``;
+``.to(device)``; and cheap pickling, because ``AmenitiesDetector.bind(model,
+processor)`` ships the bound model into every Serve replica.
+The device engine is therefore created lazily inside the replica, on its
+first call, from the host-side weight dictionary.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass
+
+import torch
+
+from .config import PRESETS, SpotterConfig
+
+
+@dataclass
+class SpotterDetectionOutput:
+    logits: torch.Tensor
+    pred_boxes: torch.Tensor
+
+    def __getitem__(self, k):
+        return getattr(self, k)
+
+
+class _Config:
+    """The bits of HF's config the caller reads (`id2label`, `num_labels`)."""
+
+    def __init__(self, cfg: SpotterConfig):
+        self.id2label = dict(cfg.id2label)
+        self.label2id = {v: k for k, v in self.id2label.items()}
+        self.num_labels = cfg.num_labels
+        self.num_queries = cfg.num_queries
+        self.model_type = "rt_detr_v2"
+        self.spotter = cfg
+
+
+def _preset_for(name: str) -> SpotterConfig:
+    n = name.lower()
+    if "r18" in n:
+        return PRESETS["r18vd"]
+    return PRESETS["r101vd"]
+
+
+class SpotterForObjectDetection:
+    main_input_name = "pixel_values"
+
+    def __init__(self, cfg: SpotterConfig, weights: dict | None = None, seed: int = 0):
+        self.cfg = cfg
+        self.config = _Config(cfg)
+        self._weights = weights
+        self._seed = seed
+        self._engine = None
+        self._device = None
+        self._lock = threading.Lock()
+
+    # -- construction -------------------------------------------------------------
+    @classmethod
+    def from_pretrained(cls, name_or_path: str = "PekingU/rtdetr_v2_r101vd", **kw):
+        """Local directory with HF weights → those weights (spotter_amd.checkpoint);
+        anything else (a hub name; no network here) → the preset's deterministic synthetic weights."""
+        if os.path.isdir(name_or_path):
+            from .checkpoint import load_local
+
+            cfg, weights = load_local(name_or_path)
+            return cls(cfg, weights)
+        return cls(_preset_for(name_or_path), None, seed=kw.get("seed", 0))
+
+    def _host_weights(self):
+        if self._weights is None:
+            from .weights import generate
+
+            self._weights = generate(self.cfg, seed=self._seed)
+        return self._weights
+
+    # -- nn.Module-ish surface ----------------------------------------------------
+    def to(self, device=None, *a, **k):
+        dev = torch.device(device) if device is not None else None
+        if dev is not None and dev.type == "cuda":
+            self._device = dev
+        return self  # cpu/mps requests (serve.py:61) keep the engine on the MI355X
+
+    def eval(self):
+        return self
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None
+        st["_lock"] = None
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self._lock = threading.Lock()
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            with self._lock:
+                if self._engine is None:
+                    from .engine import Engine
+
+                    dev = self._device or torch.device("cuda", torch.cuda.current_device())
+                    self._engine = Engine(self.cfg, self._host_weights(), dev)
+        return self._engine
+
+    # -- forward ------------------------------------------------------------------
+    def __call__(self, pixel_values=None, pixel_mask=None, **kwargs):
+        if pixel_values is None:
+            raise ValueError("You have to specify either pixel_values or inputs_embeds")
+        eng = self.engine
+        logits, boxes = eng.forward(pixel_values)
+        # own copies: the engine reuses its workspace on the next call
+        return SpotterDetectionOutput(logits=logits.clone(), pred_boxes=boxes.clone())
+
+    forward = __call__

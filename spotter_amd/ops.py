@@ -1,0 +1,217 @@
+"""Host-side wrappers of the C-ABI kernels, over torch device tensors.
+
+Every wrapper checks, on the host and before the launch, that each operand's
+addressed span lies inside its tensor's storage (a faulting kernel can take
+the whole GPU node down), then calls libspotter_hip on torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import torch
+
+from ._lib import SpConvDesc, SpImageU8, SpMsdaDesc, call
+
+ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class V:
+    """A strided row view into a float32 device tensor: rows of `ld` elements from `off`."""
+    t: torch.Tensor
+    off: int = 0
+    ld: int = 0
+
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + 4 * self.off
+
+    def need(self, rows: int, cols: int, what: str):
+        if self.t.dtype != torch.float32 or not self.t.is_cuda:
+            raise TypeError(f"{what}: expected a float32 CUDA tensor")
+        if not self.t.is_contiguous():
+            raise ValueError(f"{what}: tensor must be contiguous")
+        last = self.off + (rows - 1) * self.ld + cols if rows > 0 else self.off
+        if self.off < 0 or cols > self.ld or last > self.t.numel():
+            raise ValueError(f"{what}: span rows={rows} cols={cols} ld={self.ld} off={self.off} "
+                             f"exceeds numel={self.t.numel()}")
+        return self.ptr
+
+
+def view(t: torch.Tensor, ld: int | None = None, off: int = 0) -> V:
+    return V(t, off, ld if ld is not None else t.shape[-1])
+
+
+def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, k: int, stride: int,
+           pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
+           res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
+           rows_per_group: int = 0, group_stride: int = 0):
+    ho = (h + 2 * pad - k) // stride + 1
+    wo = (w + 2 * pad - k) // stride + 1
+    m = n * ho * wo
+    d = SpConvDesc()
+    d.A = x.need(n * h * w, cin, "conv.A")
+    d.lda = x.ld
+    if a2 is not None:
+        d.A2 = a2.need(n * h * w, cin, "conv.A2")
+        d.lda2 = a2.ld
+    d.N, d.H, d.W, d.Cin = n, h, w, cin
+    d.KH = d.KW = k
+    d.stride, d.pad, d.Ho, d.Wo = stride, pad, ho, wo
+    if wt.numel() != cout * k * k * cin or not wt.is_contiguous():
+        raise ValueError(f"conv weight numel {wt.numel()} != {cout}*{k}*{k}*{cin}")
+    d.Wt = wt.data_ptr()
+    d.Cout = cout
+    for name, t in (("scale", scale), ("shift", shift)):
+        if t is not None:
+            if t.numel() < cout:
+                raise ValueError(f"conv.{name} too short")
+            setattr(d, name, t.data_ptr())
+    if row_scale is not None:
+        d.row_scale = row_scale.data_ptr()
+        d.row_period = row_scale.numel()
+    if res1 is not None:
+        d.res1 = res1.need(m, cout, "conv.res1")
+        d.ldr1 = res1.ld
+    d.act = ACT[act]
+    if res2 is not None:
+        d.res2 = res2.need(m, cout, "conv.res2")
+        d.ldr2 = res2.ld
+    if rows_per_group:
+        groups = (m + rows_per_group - 1) // rows_per_group
+        last = out.off + (groups - 1) * group_stride + (rows_per_group - 1) * out.ld + cout
+        if last > out.t.numel() or cout > out.ld:
+            raise ValueError("conv.C grouped span exceeds output")
+        d.C = out.ptr
+    else:
+        d.C = out.need(m, cout, "conv.C")
+    d.ldc = out.ld
+    d.out_rows_per_group = rows_per_group
+    d.out_group_stride = group_stride
+    call("sp_conv2d", C.byref(d), stream())
+    return ho, wo
+
+
+def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
+           res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
+           scale=None):
+    return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
+                  res2=res2, a2=a2, row_scale=row_scale)
+
+
+def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):
+    n, c, h, w = x.shape
+    assert y.numel() >= x.numel() and x.is_contiguous()
+    call("sp_nchw_to_nhwc", x.data_ptr(), y.data_ptr(), n, c, h, w, stream())
+
+
+def maxpool3x3s2(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
+    call("sp_maxpool3x3s2", x.data_ptr(), y.data_ptr(), n, h, w, c, stream())
+    return ho, wo
+
+
+def avgpool2x2_ceil(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
+    call("sp_avgpool2x2_ceil", x.data_ptr(), y.data_ptr(), n, h, w, c, stream())
+    return ho, wo
+
+
+def upsample2x(x: V, y: V, n, h, w, c):
+    xp = x.need(n * h * w, c, "upsample.x")
+    yp = y.need(n * 4 * h * w, c, "upsample.y")
+    call("sp_upsample2x_nearest", xp, x.ld, yp, y.ld, n, h, w, c, stream())
+
+
+def layernorm(x: V, gamma, beta, y: V, rows, d, eps=1e-5):
+    xp = x.need(rows, d, "ln.x")
+    yp = y.need(rows, d, "ln.y")
+    call("sp_layernorm", xp, x.ld, gamma.data_ptr(), beta.data_ptr(), yp, y.ld, rows, d, eps, stream())
+
+
+def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale):
+    rows = batch * n
+    call("sp_attention", q.need(rows, heads * dh, "attn.q"), q.ld, k.need(rows, heads * dh, "attn.k"),
+         k.ld, v.need(rows, heads * dh, "attn.v"), v.ld, o.need(rows, heads * dh, "attn.o"), o.ld, batch,
+         n, heads, dh, scale, stream())
+
+
+def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q, heads, head_dim,
+         shapes, starts, points, offset_scale):
+    d = SpMsdaDesc()
+    L = len(shapes)
+    d.value = value.need(B * S, value_col + heads * head_dim, "msda.value")
+    d.ld_value = value.ld
+    d.value_col = value_col
+    d.off_aw = off_aw.need(B * Q, heads * L * points * 3, "msda.off_aw")
+    d.ld_off_aw = off_aw.ld
+    assert ref.numel() >= B * Q * 4
+    d.ref = ref.data_ptr()
+    d.out = out.need(B * Q, heads * head_dim, "msda.out")
+    d.ld_out = out.ld
+    d.B, d.S, d.Q, d.heads, d.head_dim, d.levels, d.points = B, S, Q, heads, head_dim, L, points
+    for i, ((h, w), s0) in enumerate(zip(shapes, starts)):
+        d.level_h[i], d.level_w[i], d.level_start[i] = h, w, s0
+    d.offset_scale = offset_scale
+    call("sp_msda", C.byref(d), stream())
+
+
+def topk_rows(x: V, rows, n, k, idx: torch.Tensor, vals: torch.Tensor | None = None, reduce_c=1,
+              apply_sigmoid=False):
+    xp = x.need(rows, n * reduce_c, "topk.x")
+    assert idx.dtype == torch.int32 and idx.numel() >= rows * k
+    if vals is not None:
+        assert vals.numel() >= rows * k
+    call("sp_topk_rows", xp, x.ld, rows, n, reduce_c, int(apply_sigmoid), k,
+         vals.data_ptr() if vals is not None else None, idx.data_ptr(), stream())
+
+
+def gather_rows(src: V, src_rows, idx: torch.Tensor, k, batch, d, dst: V):
+    sp_ = src.need(batch * src_rows, d, "gather.src")
+    dp = dst.need(batch * k, d, "gather.dst")
+    call("sp_gather_rows", sp_, src.ld, src_rows, idx.data_ptr(), k, batch, d, dp, dst.ld, stream())
+
+
+def ref_init(delta: V, anchors: torch.Tensor, idx: torch.Tensor, batch, k, ref: torch.Tensor):
+    dp = delta.need(batch * k, 4, "ref_init.delta")
+    assert ref.numel() >= batch * k * 4
+    call("sp_ref_init", dp, delta.ld, anchors.data_ptr(), idx.data_ptr(), batch, k, ref.data_ptr(), stream())
+
+
+def box_refine(delta: V, ref: torch.Tensor, rows):
+    dp = delta.need(rows, 4, "box_refine.delta")
+    assert ref.numel() >= rows * 4
+    call("sp_box_refine", dp, delta.ld, ref.data_ptr(), rows, stream())
+
+
+def preprocess_u8(images, out: torch.Tensor, out_h: int, out_w: int):
+    """images: list of uint8 CUDA tensors [H, W, 3] (contiguous)."""
+    n = len(images)
+    arr = (SpImageU8 * n)()
+    for i, im in enumerate(images):
+        assert im.dtype == torch.uint8 and im.is_cuda and im.dim() == 3 and im.shape[2] == 3
+        assert im.is_contiguous()
+        arr[i].data = im.data_ptr()
+        arr[i].height, arr[i].width = im.shape[0], im.shape[1]
+        arr[i].row_stride = im.shape[1] * 3
+    assert out.numel() >= n * 3 * out_h * out_w and out.dtype == torch.float32
+    call("sp_preprocess_u8", arr, n, out_h, out_w, out.data_ptr(), stream())
+
+
+def postprocess(logits: torch.Tensor, boxes: torch.Tensor, target_hw: torch.Tensor, k: int, threshold: float,
+                scores, labels, boxes_xyxy, counts, work):
+    b, q, c = logits.shape
+    assert logits.is_contiguous() and boxes.is_contiguous() and boxes.shape[:2] == (b, q)
+    assert target_hw.dtype == torch.int32 and target_hw.numel() >= 2 * b
+    assert scores.numel() >= b * k and labels.numel() >= b * k and labels.dtype == torch.int64
+    assert boxes_xyxy.numel() >= b * k * 4 and counts.numel() >= b and work.numel() >= b * k
+    call("sp_postprocess", logits.data_ptr(), boxes.data_ptr(), target_hw.data_ptr(), b, q, c, k, threshold,
+         scores.data_ptr(), labels.data_ptr(), boxes_xyxy.data_ptr(), counts.data_ptr(), work.data_ptr(),
+         stream())

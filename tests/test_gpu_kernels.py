@@ -1,0 +1,304 @@
+"""GPU parity of each C-ABI kernel against the CPU oracle (oracle/*.py) on seeded inputs.
+
+Integer/byte/index work must be bit-exact (preprocess, top-k, post-process
+labels); fp32 arithmetic is compared with the tolerance stated per test.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from spotter_amd._lib import lib
+
+    assert lib().sp_device_init(0) == 0, lib().sp_last_error()
+    return torch.device("cuda", 0)
+
+
+def T(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def conv_ref(x, w, stride, pad, scale, shift, act=None, res1=None, res2=None, row_scale=None):
+    from oracle.rtdetr_np import conv2d_nhwc, gelu, relu, silu
+
+    y = conv2d_nhwc(x.astype(np.float64).astype(np.float32), w, stride, pad).astype(np.float64)
+    n, ho, wo, co = y.shape
+    y = y.reshape(-1, co)
+    if row_scale is not None:
+        y = y * row_scale[np.arange(y.shape[0]) % row_scale.size][:, None]
+    y = y * scale + shift
+    if res1 is not None:
+        y = y + res1
+    y = y.astype(np.float32)
+    if act == "relu":
+        y = relu(y)
+    elif act == "silu":
+        y = silu(y)
+    elif act == "gelu":
+        y = gelu(y)
+    if res2 is not None:
+        y = y + res2
+    return y
+
+
+CONV_CASES = [
+    # n, h, w, cin, cout, k, stride, act
+    (2, 9, 11, 64, 96, 1, 1, "relu"),
+    (1, 13, 10, 32, 40, 3, 1, "silu"),
+    (2, 12, 12, 64, 64, 3, 2, None),
+    (1, 17, 15, 3, 32, 3, 2, "relu"),      # stem: Cin=3 generic path
+    (3, 5, 7, 128, 300, 1, 1, "gelu"),
+    (1, 1, 37, 4, 512, 1, 1, "relu"),      # query_pos_head layer 0 (K=4)
+    (2, 20, 20, 256, 130, 3, 1, None),     # ragged Cout
+    (1, 40, 40, 96, 256, 1, 1, "relu"),    # >= 480 tiles → 128x128 path
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_matches_oracle(dev, case):
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    n, h, w, cin, cout, k, st, act = case
+    rng = np.random.default_rng(hash(case) % 2**32)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32) * 0.1
+    pad = k // 2
+    ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+    m = n * ho * wo
+    r1 = rng.standard_normal((m, cout)).astype(np.float32)
+    r2 = rng.standard_normal((m, cout)).astype(np.float32)
+    ref = conv_ref(x, wt, st, pad, sc, sh, act, r1, r2)
+    out = torch.empty(m * cout, device=dev)
+    wk = T(wt.transpose(0, 2, 3, 1).reshape(cout, -1), dev)
+    ops.conv2d(view(T(x.reshape(-1), dev), cin), n, h, w, cin, wk, cout, k, st, pad, view(out, cout),
+               scale=T(sc, dev), shift=T(sh, dev), act=act, res1=view(T(r1.reshape(-1), dev), cout),
+               res2=view(T(r2.reshape(-1), dev), cout))
+    got = out.cpu().numpy().reshape(m, cout)
+    # fp32 MFMA (exact fmaf chains) vs BLAS fp32: reassociation only
+    np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
+
+
+def test_conv2d_strided_views_rowscale_a2_grouped(dev):
+    """lda > Cin input slice, A2 addend, row mask, grouped output rows (source_flatten write)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(7)
+    rows, K, N = 150, 64, 96
+    big = rng.standard_normal((rows, 160)).astype(np.float32)
+    a2 = rng.standard_normal((rows, K)).astype(np.float32)
+    wt = (rng.standard_normal((N, K)) / 8).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    mask = (rng.uniform(size=50) > 0.3).astype(np.float32)
+    x = big[:, 32:32 + K] + a2
+    ref = ((x @ wt.T) * mask[np.arange(rows) % 50][:, None] + b).astype(np.float32)
+    # grouped output: 3 groups of 50 rows into a [3, 70, N] buffer at row offset 11
+    out = torch.zeros(3 * 70 * N, device=dev)
+    ops.conv2d(V(T(big.reshape(-1), dev), 32, 160), 1, 1, rows, K, T(wt, dev), N, 1, 1, 0,
+               V(out, 11 * N, N), shift=T(b, dev), a2=V(T(a2.reshape(-1), dev), 0, K),
+               row_scale=T(mask, dev), rows_per_group=50, group_stride=70 * N)
+    got = out.cpu().numpy().reshape(3, 70, N)[:, 11:61].reshape(rows, N)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
+    assert np.all(out.cpu().numpy().reshape(3, 70, N)[:, :11] == 0)
+
+
+def test_pools_and_upsample_exact(dev):
+    from oracle.rtdetr_np import avgpool2_ceil, maxpool3s2, upsample2
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(3)
+    for (n, h, w, c) in [(2, 9, 7, 8), (1, 16, 16, 64), (3, 5, 6, 4)]:
+        x = rng.standard_normal((n, h, w, c)).astype(np.float32)
+        xt = T(x.reshape(-1), dev)
+        ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        y = torch.empty(n * ho * wo * c, device=dev)
+        ops.maxpool3x3s2(xt, y, n, h, w, c)
+        np.testing.assert_array_equal(y.cpu().numpy().reshape(n, ho, wo, c), maxpool3s2(x))
+        ho, wo = (h + 1) // 2, (w + 1) // 2
+        y = torch.empty(n * ho * wo * c, device=dev)
+        ops.avgpool2x2_ceil(xt, y, n, h, w, c)
+        np.testing.assert_allclose(y.cpu().numpy().reshape(n, ho, wo, c), avgpool2_ceil(x), rtol=1e-6, atol=1e-6)
+        y = torch.zeros(n * 4 * h * w * 2 * c, device=dev)
+        ops.upsample2x(V(xt, 0, c), V(y, 0, 2 * c), n, h, w, c)
+        got = y.cpu().numpy().reshape(n, 2 * h, 2 * w, 2 * c)
+        np.testing.assert_array_equal(got[..., :c], upsample2(x))
+        assert np.all(got[..., c:] == 0)
+
+
+def test_nchw_to_nhwc(dev):
+    from spotter_amd import ops
+
+    x = np.random.default_rng(1).standard_normal((2, 3, 5, 7)).astype(np.float32)
+    y = torch.empty(x.size, device=dev)
+    ops.nchw_to_nhwc(T(x, dev), y)
+    np.testing.assert_array_equal(y.cpu().numpy().reshape(2, 5, 7, 3), x.transpose(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("d", [256, 384, 1000])
+def test_layernorm(dev, d):
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    rng = np.random.default_rng(d)
+    x = (rng.standard_normal((77, d)) * 3 + 1).astype(np.float32)
+    g = rng.uniform(0.5, 1.5, d).astype(np.float32)
+    b = rng.standard_normal(d).astype(np.float32)
+    y = torch.empty(77 * d, device=dev)
+    ops.layernorm(view(T(x.reshape(-1), dev), d), T(g, dev), T(b, dev), view(y, d), 77, d)
+    mu = x.astype(np.float64).mean(-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(-1, keepdims=True)
+    ref = (x - mu) / np.sqrt(var + 1e-5) * g + b
+    np.testing.assert_allclose(y.cpu().numpy().reshape(77, d), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("n,heads,dh", [(300, 8, 32), (400, 8, 48), (70, 2, 64)])
+def test_attention(dev, n, heads, dh):
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(n)
+    B = 2
+    D = heads * dh
+    qkv = rng.standard_normal((B * n, 3 * D)).astype(np.float32)
+    out = torch.empty(B * n * D, device=dev)
+    t = T(qkv.reshape(-1), dev)
+    sc = dh ** -0.5
+    ops.attention(V(t, 0, 3 * D), V(t, D, 3 * D), V(t, 2 * D, 3 * D), V(out, 0, D), B, n, heads, dh, sc)
+    q = qkv[:, :D].reshape(B, n, heads, dh).transpose(0, 2, 1, 3).astype(np.float64)
+    k = qkv[:, D:2 * D].reshape(B, n, heads, dh).transpose(0, 2, 1, 3).astype(np.float64)
+    v = qkv[:, 2 * D:].reshape(B, n, heads, dh).transpose(0, 2, 1, 3).astype(np.float64)
+    s = q @ k.transpose(0, 1, 3, 2) * sc
+    s = np.exp(s - s.max(-1, keepdims=True))
+    a = s / s.sum(-1, keepdims=True)
+    ref = (a @ v).transpose(0, 2, 1, 3).reshape(B * n, D)
+    np.testing.assert_allclose(out.cpu().numpy().reshape(B * n, D), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_msda_matches_oracle(dev):
+    """MSDA core incl. out-of-range sampling points (zero padding) vs oracle.grid_sample_bilinear."""
+    from oracle.rtdetr_np import grid_sample_bilinear
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(11)
+    B, Q, nH, dh, nL, nP = 2, 37, 8, 32, 3, 4
+    shapes = [(16, 12), (8, 6), (4, 3)]
+    starts = [0, 192, 240]
+    S = 252
+    D = nH * dh
+    value = rng.standard_normal((B, S, 2 * D)).astype(np.float32)  # two "layers" side by side
+    offaw = np.concatenate([rng.standard_normal((B * Q, nH * nL * nP * 2)) * 2.0,
+                            rng.standard_normal((B * Q, nH * nL * nP))], 1).astype(np.float32)
+    ref = np.concatenate([rng.uniform(0.05, 0.95, (B * Q, 2)), rng.uniform(0.05, 0.6, (B * Q, 2))], 1).astype(np.float32)
+    out = torch.empty(B * Q * D, device=dev)
+    ops.msda(V(T(value.reshape(-1), dev), 0, 2 * D), D, V(T(offaw.reshape(-1), dev), 0, offaw.shape[1]),
+             T(ref, dev), V(out, 0, D), B, S, Q, nH, dh, shapes, starts, nP, 0.5)
+    # oracle (M2:200-215 + core M2:44-115)
+    off = offaw[:, :nH * nL * nP * 2].reshape(B, Q, nH, nL * nP, 2)
+    aw = offaw[:, nH * nL * nP * 2:].reshape(B, Q, nH, nL * nP).astype(np.float64)
+    aw = np.exp(aw - aw.max(-1, keepdims=True))
+    aw = aw / aw.sum(-1, keepdims=True)
+    r = ref.reshape(B, Q, 4)
+    loc = r[:, :, None, None, :2] + off * np.float32(1 / nP) * r[:, :, None, None, 2:] * np.float32(0.5)
+    vv = value[:, :, D:].reshape(B, S, nH, dh)
+    exp = np.zeros((B, nH, Q, dh))
+    for l, (h, w) in enumerate(shapes):
+        vl = vv[:, starts[l]:starts[l] + h * w].reshape(B, h, w, nH, dh).transpose(0, 3, 1, 2, 4).reshape(B * nH, h, w, dh)
+        lc = loc[:, :, :, l * nP:(l + 1) * nP].transpose(0, 2, 1, 3, 4).reshape(B * nH, Q, nP, 2)
+        sv = grid_sample_bilinear(vl, lc.astype(np.float32)).reshape(B, nH, Q, nP, dh)
+        exp += (sv * aw[:, :, :, l * nP:(l + 1) * nP].transpose(0, 2, 1, 3)[..., None]).sum(3)
+    exp = exp.transpose(0, 2, 1, 3).reshape(B * Q, D)
+    np.testing.assert_allclose(out.cpu().numpy().reshape(B * Q, D), exp, rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("n,k,reduce_c,ties", [(8400, 300, 1, False), (1000, 300, 80, False),
+                                               (24000, 300, 1, False), (5000, 300, 1, True), (300, 300, 1, True)])
+def test_topk_exact(dev, n, k, reduce_c, ties):
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(n + k)
+    rows = 3
+    if ties:
+        x = rng.integers(-20, 20, (rows, n * reduce_c)).astype(np.float32)
+    else:
+        x = rng.standard_normal((rows, n * reduce_c)).astype(np.float32)
+    idx = torch.empty(rows * k, dtype=torch.int32, device=dev)
+    vals = torch.empty(rows * k, device=dev)
+    ops.topk_rows(V(T(x.reshape(-1), dev), 0, n * reduce_c), rows, n, k, idx, vals, reduce_c=reduce_c)
+    red = x.reshape(rows, n, reduce_c).max(-1)
+    exp = np.argsort(-red, axis=-1, kind="stable")[:, :k]
+    np.testing.assert_array_equal(idx.cpu().numpy().reshape(rows, k), exp)
+    np.testing.assert_array_equal(vals.cpu().numpy().reshape(rows, k), np.take_along_axis(red, exp, 1))
+
+
+def test_postprocess_matches_oracle(dev):
+    from oracle.rtdetr_np import post_process
+    from spotter_amd import ops
+
+    rng = np.random.default_rng(5)
+    B, Q, C = 3, 300, 80
+    logits = (rng.standard_normal((B, Q, C)) - 3).astype(np.float32)
+    boxes = rng.uniform(0.05, 0.95, (B, Q, 4)).astype(np.float32)
+    ts = np.array([[717, 1200], [640, 640], [1, 3000]], np.int32)
+    sc = torch.empty(B * Q, device=dev)
+    lb = torch.empty(B * Q, dtype=torch.int64, device=dev)
+    bx = torch.empty(B * Q * 4, device=dev)
+    cnt = torch.empty(B, dtype=torch.int32, device=dev)
+    work = torch.empty(B * Q, dtype=torch.int32, device=dev)
+    ops.postprocess(T(logits, dev), T(boxes, dev), T(ts, dev), Q, 0.5, sc, lb, bx, cnt, work)
+    ref = post_process(logits, boxes, ts.tolist(), 0.5)
+    sc, lb, bx, cnt = sc.cpu().numpy().reshape(B, Q), lb.cpu().numpy().reshape(B, Q), bx.cpu().numpy().reshape(B, Q, 4), cnt.cpu().numpy()
+    for i in range(B):
+        n = cnt[i]
+        assert n == len(ref[i]["scores"])
+        np.testing.assert_array_equal(lb[i, :n], ref[i]["labels"])
+        np.testing.assert_allclose(sc[i, :n], ref[i]["scores"], rtol=0, atol=1e-7)
+        np.testing.assert_allclose(bx[i, :n], ref[i]["boxes"], rtol=1e-6, atol=1e-4)
+
+
+PRE_SIZES = [(480, 800), (333, 517), (640, 640), (300, 200), (1080, 1920), (717, 1200), (2160, 3840),
+             (1, 1), (2, 3000), (700, 640)]
+
+
+@pytest.mark.parametrize("out", [640, 1280])
+def test_preprocess_bit_exact(dev, out):
+    from oracle.pil_resize import preprocess
+    from spotter_amd import ops
+    from spotter_amd.synthetic import synthetic_image
+
+    imgs = [synthetic_image(h * 7 + w, h, w) for (h, w) in PRE_SIZES]
+    res = torch.empty(len(imgs) * 3 * out * out, device=dev)
+    ops.preprocess_u8([T(im, dev) for im in imgs], res, out, out)
+    got = res.cpu().numpy().reshape(len(imgs), 3, out, out)
+    for i, im in enumerate(imgs):
+        np.testing.assert_array_equal(got[i], preprocess(im, (out, out)), err_msg=str(PRE_SIZES[i]))
+
+
+def test_preprocess_matches_golden_digests(dev):
+    """sha256 of the HF processor's pixel_values (tests/golden/preprocess.npz) — incl. test_pic.jpg."""
+    from PIL import Image
+
+    from spotter_amd import ops
+    from spotter_amd.synthetic import synthetic_image
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "preprocess.npz"))
+    with Image.open(os.path.join(os.path.dirname(__file__), "golden", "test_pic.jpg")) as im:
+        pic = np.asarray(im.convert("RGB"))
+    for (h, w, o), seed, dig in zip(g["sizes"], g["seeds"], g["digests"]):
+        img = pic if seed < 0 else synthetic_image(int(seed), int(h), int(w))
+        res = torch.empty(3 * o * o, device=dev)
+        ops.preprocess_u8([T(img, dev)], res, int(o), int(o))
+        assert hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest() == str(dig), (h, w, o)
