@@ -1,0 +1,214 @@
+"""Throughput bench: RT-DETRv2-R101vd, 640², batch 32 per GPU, images/sec (BASELINE.json).
+
+A step = one pass of the /detect hot path over one batch of synthetic uint8
+images already resident in HBM: fused preprocess (sp_preprocess_u8) → full
+RT-DETRv2 forward → post_process_object_detection (sp_postprocess). Scaling
+is one process per GPU with no data-path collective (replicas, "weak"); a
+gloo process group only provides the barrier and the max-over-ranks time.
+
+    python bench.py [--gpus N --steps K --warmup W --batch 32 --preset r101vd --size 640]
+
+Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (the
+dominant kernel: the fp32 MFMA implicit-GEMM conv, HIP-event timed inside the
+timed region) and `cpu_baseline` (the reference HF path on the host CPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--preset", default="r101vd")
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
+    return ap.parse_args()
+
+
+class ConvEventRecorder:
+    """HIP events around every conv_gemm launch on the launch stream (torch's current stream)."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.recs = []
+
+    def __call__(self, launch, flops):
+        t = self.torch
+        e0 = t.cuda.Event(enable_timing=True)
+        e1 = t.cuda.Event(enable_timing=True)
+        e0.record()
+        launch()
+        e1.record()
+        self.recs.append((e0, e1, flops))
+
+    def summary(self):
+        ms = sum(e0.elapsed_time(e1) for e0, e1, _ in self.recs)
+        fl = sum(f for _, _, f in self.recs)
+        return ms, fl, len(self.recs)
+
+
+def cpu_baseline(cfg, weights, seconds):
+    """Reference CPU path (HF RTDetrImageProcessorPil → RTDetrV2ForObjectDetection fp32 →
+    post_process_object_detection), bs=1 as /detect runs it (serve.py:96-109), on the host cores."""
+    import numpy as np
+    import torch
+    from PIL import Image
+
+    from oracle.hf_ref import build_hf_model, build_hf_processor
+    from spotter_amd.synthetic import synthetic_image
+
+    ncores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    ncores = int(os.environ.get("OMP_NUM_THREADS", ncores))
+    torch.set_num_threads(ncores)
+    model = build_hf_model(cfg, weights)
+    proc = build_hf_processor()
+    imgs = [Image.fromarray(synthetic_image(500 + i, cfg.image_size, cfg.image_size)) for i in range(4)]
+
+    def one(im):
+        inp = proc(images=im, return_tensors="pt")
+        with torch.no_grad():
+            out = model(**inp)
+        proc.post_process_object_detection(out, target_sizes=torch.tensor([[im.size[1], im.size[0]]]),
+                                           threshold=0.5)
+
+    one(imgs[0])  # warmup
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        one(imgs[n % len(imgs)])
+        n += 1
+        if time.perf_counter() - t0 >= seconds and n >= 3:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "reference",
+            "sample": f"{n} images bs=1 {cfg.image_size}x{cfg.image_size} through HF transformers "
+                      f"RTDetrImageProcessorPil+RTDetrV2ForObjectDetection(fp32, synthetic {cfg.name} weights)"
+                      f"+post_process_object_detection on {torch.get_num_threads()} host threads, {dt:.1f}s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from spotter_amd import ops
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+    from spotter_amd.synthetic import synthetic_batch
+    from spotter_amd.weights import generate
+
+    cfg = PRESETS[args.preset].replace(image_size=args.size)
+    weights = generate(cfg, seed=0)
+    eng = Engine(cfg, weights, dev)
+    B, S = args.batch, args.size
+    imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
+    imgs = [torch.from_numpy(im).to(dev) for im in imgs_host]  # resident in HBM
+    px = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
+    K = cfg.num_queries
+    tsz = torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev)
+    scores = torch.empty((B, K), device=dev)
+    labels = torch.empty((B, K), dtype=torch.int64, device=dev)
+    boxes = torch.empty((B, K, 4), device=dev)
+    counts = torch.empty((B,), dtype=torch.int32, device=dev)
+    work = torch.empty((B, K), dtype=torch.int32, device=dev)
+
+    def step():
+        ops.preprocess_u8(imgs, px, S, S)
+        logits, pred = eng.forward(px)
+        ops.postprocess(logits, pred, tsz, K, 0.5, scores, labels, boxes, counts, work)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    rec = None if args.no_events else ConvEventRecorder(torch)
+    ops.set_conv_hook(rec)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    ops.set_conv_hook(None)
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_img = world * B * args.steps
+    value = n_img / elapsed
+
+    roof = None
+    if rec is not None and rec.recs:
+        ms, fl, nl = rec.summary()
+        per_launch_ms = ms / nl
+        ach = fl / (ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)",
+                "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "launches_per_step": nl // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
+                "gflop_per_step": round(fl / args.steps / 1e9, 2),
+                "kernel_ms_per_step": round(ms / args.steps, 3)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(cfg, weights, args.cpu_baseline_seconds)
+        except Exception as e:  # keep the GPU line even if the host path is unavailable
+            cpu = {"value": None, "unit": "images/sec", "cores": None, "kind": "reference",
+                   "sample": f"unavailable: {type(e).__name__}: {e}"}
+
+    if rank == 0:
+        line = {
+            "metric": "images/sec RT-DETRv2-R101 640² bs32 (per GPU, replicas)" if args.preset == "r101vd"
+            else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B}",
+            "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic uint8 RGB images (seeded), synthetic deterministic weights",
+            "config": {"workload": f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess",
+                       "model": f"rtdetr_v2_{args.preset}", "global_batch": B * world, "image_size": S,
+                       "parallelism": f"replicas x{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,14 @@ from ._lib import SpConvDesc, SpImageU8, SpMsdaDesc, call
 
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
 
+_conv_hook = None
+
+
+def set_conv_hook(hook):
+    """hook(launch: callable, flops: int) wraps every conv/linear launch (bench.py HIP-event timing)."""
+    global _conv_hook
+    _conv_hook = hook
+
 
 def stream() -> int:
     return torch.cuda.current_stream().cuda_stream
@@ -93,7 +101,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     d.ldc = out.ld
     d.out_rows_per_group = rows_per_group
     d.out_group_stride = group_stride
-    call("sp_conv2d", C.byref(d), stream())
+    if _conv_hook is None:
+        call("sp_conv2d", C.byref(d), stream())
+    else:
+        _conv_hook(lambda: call("sp_conv2d", C.byref(d), stream()), 2 * m * cout * k * k * cin)
     return ho, wo
 
 
