@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
     return ap.parse_args()
 
 
@@ -48,18 +49,29 @@ class ConvEventRecorder:
         self.torch = torch
         self.recs = []
 
-    def __call__(self, launch, flops):
+    def __call__(self, launch, flops, shape=None):
         t = self.torch
         e0 = t.cuda.Event(enable_timing=True)
         e1 = t.cuda.Event(enable_timing=True)
         e0.record()
         launch()
         e1.record()
-        self.recs.append((e0, e1, flops))
+        self.recs.append((e0, e1, flops, shape))
+
+    def by_shape(self):
+        agg = {}
+        for e0, e1, f, shp in self.recs:
+            a = agg.setdefault(str(shp), [0, 0.0, 0])
+            a[0] += 1
+            a[1] += e0.elapsed_time(e1)
+            a[2] += f
+        rows = [{"shape(M,N,K,k,s)": k, "launches": v[0], "ms": round(v[1], 3),
+                 "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1)} for k, v in agg.items()]
+        return sorted(rows, key=lambda r: -r["ms"])
 
     def summary(self):
-        ms = sum(e0.elapsed_time(e1) for e0, e1, _ in self.recs)
-        fl = sum(f for _, _, f in self.recs)
+        ms = sum(r[0].elapsed_time(r[1]) for r in self.recs)
+        fl = sum(r[2] for r in self.recs)
         return ms, fl, len(self.recs)
 
 
@@ -122,6 +134,7 @@ def main():
     from spotter_amd.config import PRESETS
     from spotter_amd.engine import Engine
     from spotter_amd.synthetic import synthetic_batch
+    from spotter_amd.replicas import barrier, max_over_ranks
     from spotter_amd.weights import generate
 
     cfg = PRESETS[args.preset].replace(image_size=args.size)
@@ -151,10 +164,6 @@ def main():
     rec = None if args.no_events else ConvEventRecorder(torch)
     ops.set_conv_hook(rec)
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -165,10 +174,7 @@ def main():
     barrier()
     ops.set_conv_hook(None)
     elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
     n_img = world * B * args.steps
     value = n_img / elapsed
 
@@ -183,6 +189,10 @@ def main():
                 "launches_per_step": nl // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
                 "gflop_per_step": round(fl / args.steps / 1e9, 2),
                 "kernel_ms_per_step": round(ms / args.steps, 3)}
+
+    if rec is not None and args.detail and rank == 0:
+        with open(args.detail, "w") as f:
+            json.dump(rec.by_shape(), f, indent=1)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

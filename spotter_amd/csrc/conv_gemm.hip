@@ -21,6 +21,8 @@
 // BatchNorm scale/shift (FrozenBN M2:748-758 / eval BN), residual, activation,
 // post-activation residual, and a grouped output row map so projections write
 // straight into concatenated / flattened buffers (M2:1553-1555).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace sp {
@@ -36,7 +38,8 @@ struct ConvArgs {
   int64_t M;
   int32_t K;
   int32_t HoWo;
-  int32_t fast;  // Cin % 32 == 0
+  int32_t fast;     // Cin % 32 == 0 and 16-byte aligned operands
+  int32_t vec_epi;  // 16-byte aligned C/res/scale/shift rows → float4 epilogue
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 2); }
@@ -48,15 +51,16 @@ __device__ __forceinline__ float act_apply(float v, int act) {
   return v;
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int DB>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   constexpr int BM = 64 * TM;
   constexpr int BN = 64 * TN;
   constexpr int PA = BM / 32;  // loader passes (32 rows per pass)
   constexpr int PB = BN / 32;
-  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * BK];
-  float* As = smem;
-  float* Bs = smem + BM * BK;
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int EPI = 4 * 32 * (TN * 32);  // epilogue: one 32×(32·TN) slab per wave
+  constexpr int SMEM = STAGE * (DB ? 2 : 1) > EPI ? STAGE * (DB ? 2 : 1) : EPI;
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
 
   const sp_conv_desc& d = p.d;
   const int tid = threadIdx.x;
@@ -168,17 +172,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
   const int nk = (p.K + BK - 1) / BK;
-  load_tile(0);
-  for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();
+
+  auto store_tile = [&](float* st) {
+    float* As = st;
+    float* Bs = st + BM * BK;
 #pragma unroll
     for (int i = 0; i < PA; ++i)
       *reinterpret_cast<float4*>(As + swz(i * 32 + lrow, lchunk)) = ra[i];
 #pragma unroll
     for (int i = 0; i < PB; ++i)
       *reinterpret_cast<float4*>(Bs + swz(i * 32 + lrow, lchunk)) = rb[i];
-    __syncthreads();
-    if (kt + 1 < nk) load_tile(kt + 1);
+  };
+
+  auto compute_tile = [&](const float* st) {
+    const float* As = st;
+    const float* Bs = st + BM * BK;
 #pragma unroll
     for (int s = 0; s < BK / 8; ++s) {
       float4 fa[TM], fb[TN];
@@ -198,42 +206,112 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
         }
     }
+  };
+
+  load_tile(0);
+  if (DB) {
+    // two LDS stages, one barrier per k-tile: tile t+1's global loads and LDS
+    // store overlap tile t's MFMAs.
+    store_tile(smem);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load_tile(kt + 1);
+      compute_tile(smem + (kt & 1) * STAGE);
+      if (kt + 1 < nk) store_tile(smem + ((kt + 1) & 1) * STAGE);
+      __syncthreads();
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();
+      store_tile(smem);
+      __syncthreads();
+      if (kt + 1 < nk) load_tile(kt + 1);
+      compute_tile(smem);
+    }
   }
 
-  // Epilogue. acc[i][j][q] is (row (q&3) + 8*(q>>2) + 4*h, col r) of 32×32 subtile (i, j).
+  // Epilogue, staged through LDS so every lane applies it to a contiguous float4
+  // of one output row (16-byte loads of res1/res2/scale/shift, 16-byte stores):
+  // pass i moves each wave's 32-row band acc[i][*] to its private LDS slab.
+  constexpr int WN = TN * 32;  // columns per wave; LDS rows of WN floats (one bank row at TN=2)
+  float* slab = smem + wave * (32 * WN);
   const int rpg = d.out_rows_per_group > 0 ? d.out_rows_per_group : 0x7fffffff;
+  const int nb = n0 + wn * WN;
+  __syncthreads();  // main loop done with the operand stages
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * TN * 32 + j * 32 + r;
-    if (n >= d.Cout) continue;
-    const float sc = d.scale ? d.scale[n] : 1.0f;
-    const float sh = d.shift ? d.shift[n] : 0.0f;
+  for (int i = 0; i < TM; ++i) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int64_t m = m0 + wm * TM * 32 + i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (m >= p.M) continue;
-        float v = acc[i][j][q];
-        if (d.row_scale) v *= d.row_scale[m % d.row_period];
-        v = fmaf(v, sc, sh);
-        if (d.res1) v += d.res1[m * d.ldr1 + n];
-        v = act_apply(v, d.act);
-        if (d.res2) v += d.res2[m * d.ldr2 + n];
-        const int64_t g = m / rpg;
-        const int64_t rr = m - g * rpg;
-        d.C[g * d.out_group_stride + rr * d.ldc + n] = v;
+      for (int q = 0; q < 16; ++q)
+        slab[((q & 3) + 8 * (q >> 2) + 4 * h) * WN + j * 32 + r] = acc[i][j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+    __builtin_amdgcn_wave_barrier();
+    const int64_t mb = m0 + wm * TM * 32 + i * 32;
+#pragma unroll
+    for (int t = 0; t < (32 * WN / 4) / 64; ++t) {
+      const int c = lane + 64 * t;
+      const int row = c / (WN / 4);
+      const int col = (c - row * (WN / 4)) * 4;
+      const int64_t m = mb + row;
+      const int n = nb + col;
+      if (m >= p.M || n >= d.Cout) continue;
+      float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
+      const int64_t g = m / rpg;
+      const int64_t rr = m - g * rpg;
+      float* crow = d.C + g * d.out_group_stride + rr * d.ldc;
+      if (p.vec_epi && n + 3 < d.Cout) {
+        if (d.row_scale) {
+          const float rs = d.row_scale[m % d.row_period];
+          v.x *= rs; v.y *= rs; v.z *= rs; v.w *= rs;
+        }
+        float4 sc = d.scale ? *reinterpret_cast<const float4*>(d.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+        float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y);
+        v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
+        if (d.res1) {
+          float4 a = *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n);
+          v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+        }
+        v.x = act_apply(v.x, d.act); v.y = act_apply(v.y, d.act);
+        v.z = act_apply(v.z, d.act); v.w = act_apply(v.w, d.act);
+        if (d.res2) {
+          float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
+          v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+        }
+        *reinterpret_cast<float4*>(crow + n) = v;
+      } else {
+        float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int nn = n + u;
+          if (nn >= d.Cout) break;
+          float x = e[u];
+          if (d.row_scale) x *= d.row_scale[m % d.row_period];
+          x = fmaf(x, d.scale ? d.scale[nn] : 1.0f, d.shift ? d.shift[nn] : 0.0f);
+          if (d.res1) x += d.res1[m * d.ldr1 + nn];
+          x = act_apply(x, d.act);
+          if (d.res2) x += d.res2[m * d.ldr2 + nn];
+          crow[nn] = x;
+        }
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-template <int TM, int TN>
+template <int TM, int TN, int DB>
 int launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 64 * TM, BN = 64 * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM));
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB>), grid, dim3(256), 0, s, a);
   return check_launch("sp_conv2d");
+}
+
+// Tile override for tuning: SP_CONV_CFG = "<TM><TN><DB>", e.g. "221".
+int forced_cfg() {
+  const char* e = getenv("SP_CONV_CFG");
+  return e ? atoi(e) : -1;
 }
 
 }  // namespace
@@ -267,11 +345,31 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
                     (!d->A2 || ((d->lda2 % 4 == 0) && ((reinterpret_cast<uintptr_t>(d->A2) & 15) == 0)));
     if (!al) a.fast = 0;
   }
+  {
+    auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+    bool v = (d->ldc % 4 == 0) && al16(d->C) && (d->Cout % 4 == 0);
+    v = v && (!d->res1 || (d->ldr1 % 4 == 0 && al16(d->res1)));
+    v = v && (!d->res2 || (d->ldr2 % 4 == 0 && al16(d->res2)));
+    v = v && (!d->scale || al16(d->scale)) && (!d->shift || al16(d->shift));
+    v = v && (d->out_rows_per_group == 0 || d->out_group_stride % 4 == 0);
+    a.vec_epi = v ? 1 : 0;
+  }
   hipStream_t s = as_stream(stream);
-  const int64_t mt128 = (a.M + 127) / 128;
-  const int nt128 = (d->Cout + 127) / 128;
-  const int nt64 = (d->Cout + 63) / 64;
-  if (d->Cout > 64 && mt128 * nt128 >= 480) return launch<2, 2>(a, s);
-  if (mt128 * nt64 >= 480) return launch<2, 1>(a, s);
-  return launch<1, 1>(a, s);
+  switch (forced_cfg()) {
+    case 220: return launch<2, 2, 0>(a, s);
+    case 221: return launch<2, 2, 1>(a, s);
+    case 210: return launch<2, 1, 0>(a, s);
+    case 211: return launch<2, 1, 1>(a, s);
+    case 120: return launch<1, 2, 0>(a, s);
+    case 121: return launch<1, 2, 1>(a, s);
+    case 110: return launch<1, 1, 0>(a, s);
+    case 111: return launch<1, 1, 1>(a, s);
+    default: break;
+  }
+  // Tile choice (measured on MI355X, tools/conv_bench.py): the kernel is latency-bound, so
+  // occupancy beats operand reuse except for long-K, wide-N, tall-M convs.
+  const int64_t tiles64 = ((a.M + 63) / 64) * ((d->Cout + 63) / 64);
+  if (a.K >= 3000 && d->Cout >= 384 && a.M >= 100000) return launch<2, 2, 0>(a, s);
+  if (a.K <= 128 || d->Cout <= 64 || tiles64 < 3000) return launch<1, 1, 0>(a, s);
+  return launch<1, 2, 0>(a, s);
 }

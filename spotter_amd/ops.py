@@ -19,7 +19,7 @@ _conv_hook = None
 
 
 def set_conv_hook(hook):
-    """hook(launch: callable, flops: int) wraps every conv/linear launch (bench.py HIP-event timing)."""
+    """hook(launch: callable, flops: int, shape: (M, N, K, k, stride)) wraps every conv/linear launch (bench.py HIP-event timing)."""
     global _conv_hook
     _conv_hook = hook
 
@@ -104,7 +104,8 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     if _conv_hook is None:
         call("sp_conv2d", C.byref(d), stream())
     else:
-        _conv_hook(lambda: call("sp_conv2d", C.byref(d), stream()), 2 * m * cout * k * k * cin)
+        _conv_hook(lambda: call("sp_conv2d", C.byref(d), stream()), 2 * m * cout * k * k * cin,
+                   (m, cout, k * k * cin, k, stride))
     return ho, wo
 
 

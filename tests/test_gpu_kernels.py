@@ -89,6 +89,14 @@ def test_conv2d_matches_oracle(dev, case):
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
 
 
+@pytest.mark.parametrize("cfg", ["220", "221", "210", "211", "120", "121", "110", "111"])
+def test_conv2d_every_tile_config(dev, cfg, monkeypatch):
+    """Each tile variant (SP_CONV_CFG override) on a ragged 3×3 and a 1×1 with residuals."""
+    monkeypatch.setenv("SP_CONV_CFG", cfg)
+    for case in [(2, 11, 9, 64, 136, 3, 1, "silu"), (1, 7, 13, 96, 72, 1, 1, "relu"), (1, 9, 9, 3, 32, 3, 2, None)]:
+        test_conv2d_matches_oracle(dev, case)
+
+
 def test_conv2d_strided_views_rowscale_a2_grouped(dev):
     """lda > Cin input slice, A2 addend, row mask, grouped output rows (source_flatten write)."""
     from spotter_amd import ops
