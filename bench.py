@@ -39,6 +39,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
+    ap.add_argument("--microbatches", type=int, default=2, help="concurrent per-GPU batch slices (streams)")
     return ap.parse_args()
 
 
@@ -48,6 +49,8 @@ class ConvEventRecorder:
     def __init__(self, torch):
         self.torch = torch
         self.recs = []
+        self.t0 = torch.cuda.Event(enable_timing=True)
+        self.t0.record()
 
     def __call__(self, launch, flops, shape=None):
         t = self.torch
@@ -70,9 +73,22 @@ class ConvEventRecorder:
         return sorted(rows, key=lambda r: -r["ms"])
 
     def summary(self):
-        ms = sum(r[0].elapsed_time(r[1]) for r in self.recs)
+        """(sum of launch durations, union of launch intervals, flops, launches) — launches of the
+        concurrent micro-batch streams overlap, so achieved TFLOP/s uses the busy-time union."""
+        ivs = sorted((self.t0.elapsed_time(r[0]), self.t0.elapsed_time(r[1])) for r in self.recs)
+        ms = sum(b - a for a, b in ivs)
+        union, cur_a, cur_b = 0.0, None, None
+        for a, b in ivs:
+            if cur_b is None or a > cur_b:
+                if cur_b is not None:
+                    union += cur_b - cur_a
+                cur_a, cur_b = a, b
+            else:
+                cur_b = max(cur_b, b)
+        if cur_b is not None:
+            union += cur_b - cur_a
         fl = sum(r[2] for r in self.recs)
-        return ms, fl, len(self.recs)
+        return ms, union, fl, len(self.recs)
 
 
 def cpu_baseline(cfg, weights, seconds):
@@ -140,6 +156,7 @@ def main():
     cfg = PRESETS[args.preset].replace(image_size=args.size)
     weights = generate(cfg, seed=0)
     eng = Engine(cfg, weights, dev)
+    eng.microbatches = args.microbatches
     B, S = args.batch, args.size
     imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
     imgs = [torch.from_numpy(im).to(dev) for im in imgs_host]  # resident in HBM
@@ -180,15 +197,17 @@ def main():
 
     roof = None
     if rec is not None and rec.recs:
-        ms, fl, nl = rec.summary()
+        ms, busy, fl, nl = rec.summary()
         per_launch_ms = ms / nl
-        ach = fl / (ms * 1e-3) / 1e12
+        ach = fl / (busy * 1e-3) / 1e12
         roof = {"bound": "mfma", "kernel": "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)",
                 "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                 "launches_per_step": nl // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
                 "gflop_per_step": round(fl / args.steps / 1e9, 2),
-                "kernel_ms_per_step": round(ms / args.steps, 3)}
+                "conv_busy_ms_per_step": round(busy / args.steps, 3),
+                "note": "achieved = algorithmic conv/linear FLOPs / wall time with >=1 conv_gemm launch in flight "
+                        "(HIP events on the launch streams; micro-batch streams overlap)"}
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:

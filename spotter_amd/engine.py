@@ -105,10 +105,12 @@ def anchors_for(shapes, grid_size=0.05):
 class Engine:
     """Owns the packed device weights and the per-shape workspaces of one GPU."""
 
-    def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda"):
+    def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
+                 fold_repvgg: bool = True):
         from ._lib import lib
 
         self.cfg = cfg
+        self.fold_repvgg = fold_repvgg
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -121,6 +123,9 @@ class Engine:
             self._pack(weights)
         self._ws = {}
         self._consts = {}
+        self._ctxs = {}
+        self._outs = {}
+        self.microbatches = 2
 
     # ------------------------------------------------------------------ weights
     def _conv(self, p, conv_key, bn_pre, frozen):
@@ -210,9 +215,24 @@ class Engine:
         c2 = self._conv(p, pre + ".conv2.conv.weight", pre + ".conv2.norm", False)
         c12 = ConvW(torch.cat([c1.w, c2.w], 0).contiguous(), c1.cin, c1.cout + c2.cout, 1,
                     torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous())
-        reps = [(self._conv(p, f"{pre}.bottlenecks.{b}.conv1.conv.weight", f"{pre}.bottlenecks.{b}.conv1.norm", False),
-                 self._conv(p, f"{pre}.bottlenecks.{b}.conv2.conv.weight", f"{pre}.bottlenecks.{b}.conv2.norm", False))
-                for b in range(3)]
+        reps = []
+        for b in range(3):
+            q = f"{pre}.bottlenecks.{b}"
+            if self.fold_repvgg:
+                # RepVGG re-parameterisation (M2:921-923): BN1(conv3x3(x)) + BN2(conv1x1(x)) is one 3×3
+                # conv whose weights are s1·W3 with s2·W1 added to the centre tap, shift b1 + b2.
+                w3, w1 = p[q + ".conv1.conv.weight"], p[q + ".conv2.conv.weight"]
+                s1, b1 = eval_bn_affine(p, q + ".conv1.norm")
+                s2, b2 = eval_bn_affine(p, q + ".conv2.norm")
+                wf = (w3.astype(np.float64) * s1[:, None, None, None]).copy()
+                wf[:, :, 1, 1] += w1[:, :, 0, 0].astype(np.float64) * s2[:, None]
+                co, ci = w3.shape[:2]
+                reps.append(("fold", ConvW(_t(conv_khwc(wf.astype(np.float32)), self.dev), ci, co, 3,
+                                           _t(np.ones(co, np.float32), self.dev),
+                                           _t((b1.astype(np.float64) + b2).astype(np.float32), self.dev))))
+            else:
+                reps.append((self._conv(p, q + ".conv1.conv.weight", q + ".conv1.norm", False),
+                             self._conv(p, q + ".conv2.conv.weight", q + ".conv2.norm", False)))
         c3 = None
         if (pre + ".conv3.conv.weight") in p:
             c3 = self._conv(p, pre + ".conv3.conv.weight", pre + ".conv3.norm", False)
@@ -292,6 +312,7 @@ class Engine:
                 self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act="relu")
                 self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act="relu", res1=res)
             cur, h, w, c = out, ho, wo, cout
+            yield
         feats.append((cur, h, w, c))
         return feats[-3:] if nstage >= 3 else feats
 
@@ -302,16 +323,19 @@ class Engine:
         self._cv(x, B, h, w, cs["c12"], 1, view(c12, 2 * hid), act="silu")
         h2 = V(c12, hid, 2 * hid)
         cur = V(c12, 0, 2 * hid)
-        t = self._buf(f"{tag}_t", B, h, w, hid)
+        t = None if self.fold_repvgg else self._buf(f"{tag}_t", B, h, w, hid)
         final_to_out = cs["c3"] is None
         for b, (k3, k1) in enumerate(cs["reps"]):
             last = b == len(cs["reps"]) - 1
-            self._cv(cur, B, h, w, k3, 1, view(t, hid))
             if last and final_to_out:
                 dst = out
             else:
                 dst = view(self._buf(f"{tag}_r{b % 2}", B, h, w, hid), hid)
-            self._cv(cur, B, h, w, k1, 1, dst, act="silu", res1=view(t, hid), res2=h2 if last else None)
+            if k3 == "fold":
+                self._cv(cur, B, h, w, k1, 1, dst, act="silu", res2=h2 if last else None)
+            else:
+                self._cv(cur, B, h, w, k3, 1, view(t, hid))
+                self._cv(cur, B, h, w, k1, 1, dst, act="silu", res1=view(t, hid), res2=h2 if last else None)
             cur = dst
         if cs["c3"] is not None:
             self._cv(cur, B, h, w, cs["c3"], 1, out, act="silu")
@@ -353,19 +377,23 @@ class Engine:
         self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act="gelu")
         self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(t2, Hd), res1=view(y1, Hd))
         ops.layernorm(view(t2, Hd), *A["ln2"], view(p5a, Hd), rows, Hd, cfg.layer_norm_eps)
+        yield
         # FPN (M2:1183-1197)
         self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act="silu")
         ops.upsample2x(V(catn5, Hd, 2 * Hd), V(cat4, 0, 2 * Hd), B, h2, w2, Hd)
         F4 = self._buf("F4", B, h1, w1, Hd)
         self._csp_fwd(self.fpn[0], view(cat4, 2 * Hd), B, h1, w1, view(F4, Hd), "fpn0")
+        yield
         self._cv(view(F4, Hd), B, h1, w1, self.lateral[1], 1, V(catn4, Hd, 2 * Hd), act="silu")
         ops.upsample2x(V(catn4, Hd, 2 * Hd), V(cat3, 0, 2 * Hd), B, h1, w1, Hd)
         F3 = self._buf("F3", B, h0, w0, Hd)
         self._csp_fwd(self.fpn[1], view(cat3, 2 * Hd), B, h0, w0, view(F3, Hd), "fpn1")
+        yield
         # PAN (M2:1199-1207)
         self._cv(view(F3, Hd), B, h0, w0, self.down[0], 2, V(catn4, 0, 2 * Hd), act="silu")
         N4 = self._buf("N4", B, h1, w1, Hd)
         self._csp_fwd(self.pan[0], view(catn4, 2 * Hd), B, h1, w1, view(N4, Hd), "pan0")
+        yield
         self._cv(view(N4, Hd), B, h1, w1, self.down[1], 2, V(catn5, 0, 2 * Hd), act="silu")
         N5 = self._buf("N5", B, h2, w2, Hd)
         self._csp_fwd(self.pan[1], view(catn5, 2 * Hd), B, h2, w2, view(N5, Hd), "pan1")
@@ -386,8 +414,14 @@ class Engine:
                      rows_per_group=h * w, group_stride=S * D)
         return src, shapes, starts, S
 
-    def forward(self, pixel_values: torch.Tensor):
-        """pixel_values [B,3,H,W] fp32 (device) → (logits [B,Q,C], pred_boxes [B,Q,4]) (M2:1864-1881)."""
+    def forward(self, pixel_values: torch.Tensor, microbatches: int | None = None):
+        """pixel_values [B,3,H,W] fp32 (device) → (logits [B,Q,C], pred_boxes [B,Q,4]) (M2:1864-1881).
+
+        The batch is split into `microbatches` independent slices (images never interact), each
+        with its own workspace and HIP stream; their launches are interleaved block by block so
+        one slice's GEMMs fill the other's wave-quantisation tails. The returned tensors are
+        engine-owned and overwritten by the next call.
+        """
         cfg = self.cfg
         if pixel_values.device != self.dev:
             pixel_values = pixel_values.to(self.dev, non_blocking=True)
@@ -397,15 +431,66 @@ class Engine:
         B, C, H, W = pixel_values.shape
         if C != 3:
             raise ValueError("Make sure that the channel dimension of the pixel values match with the one set in the configuration.")
+        nmb = self.microbatches if microbatches is None else microbatches
+        nmb = max(1, min(nmb, B))
+        Q, NC = cfg.num_queries, cfg.num_labels
         with torch.cuda.device(self.dev):
-            px = self._buf("px_nhwc", B, H, W, 3)
-            ops.nchw_to_nhwc(pixel_values, px)
-            feats = self.backbone(px, B, H, W)
-            enc = self.encoder(feats, B)
-            src, shapes, starts, S = self.decoder_inputs(enc, B)
-            return self.decode(src, shapes, starts, S, B)
+            out_logits = self._out("logits", B * Q * NC).view(B, Q, NC)
+            out_boxes = self._out("boxes", B * Q * 4).view(B, Q, 4)
+            if nmb == 1:
+                for _ in self._run(pixel_values, out_logits, out_boxes):
+                    pass
+                return out_logits, out_boxes
+            main = torch.cuda.current_stream()
+            bounds = [B * i // nmb for i in range(nmb + 1)]
+            jobs = []
+            for i in range(nmb):
+                ctx = self._ctx(i)
+                ctx["stream"].wait_stream(main)
+                b0, b1 = bounds[i], bounds[i + 1]
+                jobs.append([ctx, self._run(pixel_values[b0:b1], out_logits[b0:b1], out_boxes[b0:b1])])
+            saved = self._ws
+            try:
+                while jobs:
+                    for job in list(jobs):
+                        ctx, g = job
+                        self._ws = ctx["ws"]
+                        with torch.cuda.stream(ctx["stream"]):
+                            try:
+                                next(g)
+                            except StopIteration:
+                                jobs.remove(job)
+            finally:
+                self._ws = saved
+            for i in range(nmb):
+                main.wait_stream(self._ctx(i)["stream"])
+            return out_logits, out_boxes
 
-    def decode(self, src, shapes, starts, S, B):
+    def _ctx(self, i):
+        c = self._ctxs.get(i)
+        if c is None:
+            c = {"ws": {}, "stream": torch.cuda.Stream(self.dev)}
+            self._ctxs[i] = c
+        return c
+
+    def _out(self, key, n):
+        t = self._outs.get(key)
+        if t is None or t.numel() < n:
+            t = torch.empty(n, dtype=torch.float32, device=self.dev)
+            self._outs[key] = t
+        return t[:n]
+
+    def _run(self, pixel_values, out_logits, out_boxes):
+        B, C, H, W = pixel_values.shape
+        px = self._buf("px_nhwc", B, H, W, 3)
+        ops.nchw_to_nhwc(pixel_values, px)
+        feats = yield from self.backbone(px, B, H, W)
+        enc = yield from self.encoder(feats, B)
+        src, shapes, starts, S = self.decoder_inputs(enc, B)
+        yield
+        yield from self.decode(src, shapes, starts, S, B, out_logits, out_boxes)
+
+    def decode(self, src, shapes, starts, S, B, out_logits, out_boxes):
         cfg = self.cfg
         D, Q, NC = cfg.d_model, cfg.num_queries, cfg.num_labels
         # query selection (M2:1582-1623)
@@ -429,7 +514,7 @@ class Engine:
         self._lin_op(view(h, D), Bq, self.enc_bbox[0], view(t_a, D), act="relu")
         self._lin_op(view(t_a, D), Bq, self.enc_bbox[1], view(t_b, D), act="relu")
         self._lin_op(view(t_b, D), Bq, self.enc_bbox[2], view(delta, 4))
-        ref = self._buf("dec_ref", Bq, 4)
+        ref = out_boxes.reshape(-1)  # refined in place, layer by layer
         ops.ref_init(view(delta, 4), anchors, topk, B, Q, ref)
         # all six value projections at once (M2:190)
         L = cfg.decoder_layers
@@ -445,7 +530,6 @@ class Engine:
         tmp = self._buf("dec_tmp", Bq, D)
         offaw = self._buf("dec_offaw", Bq, nH * nL * nP * 3)
         ff = self._buf("dec_ff", Bq, cfg.decoder_ffn_dim)
-        logits = self._buf("logits", B, Q, NC)
         for j, P in enumerate(self.dec):
             self._lin_op(view(ref, 4), Bq, self.qpos[0], view(qp, 2 * D), act="relu")
             self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
@@ -472,5 +556,5 @@ class Engine:
             self._lin_op(view(t_a, D), Bq, b1, view(t_b, D), act="relu")
             self._lin_op(view(t_b, D), Bq, b2, view(delta, 4))
             ops.box_refine(view(delta, 4), ref, Bq)
-        self._lin_op(view(h, D), Bq, self.cls_last, view(logits, NC))
-        return logits.view(B, Q, NC), ref.view(B, Q, 4)
+            yield
+        self._lin_op(view(h, D), Bq, self.cls_last, view(out_logits.reshape(-1), NC))

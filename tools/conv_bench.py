@@ -61,8 +61,10 @@ def bench_one(dev, shape, cfg):
 
 def main():
     dev = torch.device("cuda", 0)
-    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 else [None]
-    for shape in SHAPES:
+    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 and sys.argv[1] != "-" else [None]
+    which = [int(i) for i in sys.argv[2].split(",")] if len(sys.argv) > 2 else range(len(SHAPES))
+    for si in which:
+        shape = SHAPES[si]
         for cfg in cfgs:
             print(json.dumps(bench_one(dev, shape, cfg)), flush=True)
 
