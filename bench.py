@@ -39,7 +39,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
-    ap.add_argument("--microbatches", type=int, default=2, help="concurrent per-GPU batch slices (streams)")
+    ap.add_argument("--microbatches", type=int, default=1,
+                    help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, +2%%,
+                         but then per-launch durations overlap)")
     return ap.parse_args()
 
 

@@ -64,7 +64,7 @@ def make_preprocess():
                         seeds=np.array(rec["seeds"]), digests=np.array(rec["digests"]))
 
 
-def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=None):
+def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=None, src_sizes=None):
     import torch
     from PIL import Image
 
@@ -79,10 +79,13 @@ def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=No
     model = build_hf_model(cfg, w)
     pp = build_hf_processor()
     pp.size = {"height": size, "width": size}
-    imgs = [synthetic_image(s, size, size) for s in seeds]
+    src_sizes = list(src_sizes or [(size, size)] * len(seeds))
+    imgs = [synthetic_image(s, h, w) for s, (h, w) in zip(seeds, src_sizes)]
     if with_pic:
         imgs.append(load_test_pic())
-    out = {"seeds": np.array(list(seeds) + ([-1] if with_pic else [])), "size": size}
+        src_sizes.append(imgs[-1].shape[:2])
+    out = {"seeds": np.array(list(seeds) + ([-1] if with_pic else [])), "size": size,
+           "src_sizes": np.array(src_sizes)}
     hooks = {}
     model.model.enc_score_head.register_forward_hook(
         lambda m, i, o: hooks.__setitem__("enc_cls", o.detach().numpy()))
@@ -125,7 +128,9 @@ def main(argv):
     if "r101vd" in what:
         make_model("r101vd")
     if "r101vd_1280" in what:
-        make_model("r101vd", size=1280, seeds=(0,), with_pic=True, tag="r101vd_1280")
+        # C5: mixed-resolution stream resized on the GPU to 1280²
+        make_model("r101vd", size=1280, seeds=(0, 1), with_pic=True, tag="r101vd_1280",
+                   src_sizes=[(720, 1280), (1080, 1920)])
 
 
 if __name__ == "__main__":

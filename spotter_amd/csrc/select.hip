@@ -8,7 +8,7 @@
 //
 // One 1024-thread workgroup per row: keys (order-preserving uint32 of the
 // fp32 value, after the optional max-over-C reduction / sigmoid) live in LDS
-// (≤ 24,576 per row); four 8-bit radix passes find the k-th largest key T;
+// (≤ 36,864 per row); four 8-bit radix passes find the k-th largest key T;
 // keys > T are compacted, keys == T are taken in index order; a bitonic sort on
 // (key desc, index asc) orders the k winners. Deterministic.
 #include "common.h"
@@ -17,7 +17,7 @@ namespace sp {
 namespace {
 
 constexpr int kThreads = 1024;
-constexpr int kMaxN = 24576;
+constexpr int kMaxN = 36864;  // 144 KiB of keys: covers S = 33,600 at 1280² (LDS 160 KiB)
 constexpr int kMaxK = 512;
 
 __device__ __forceinline__ uint32_t f2key(float f) {

@@ -26,13 +26,14 @@ def load_images(g):
     from spotter_amd.synthetic import synthetic_image
 
     size = int(g["size"])
+    srcs = g["src_sizes"] if "src_sizes" in g.files else [(size, size)] * len(g["seeds"])
     out = []
-    for s in g["seeds"]:
+    for s, (h, w) in zip(g["seeds"], srcs):
         if s < 0:
             with Image.open(os.path.join(GOLD, "test_pic.jpg")) as im:
                 out.append(im.convert("RGB"))
         else:
-            out.append(Image.fromarray(synthetic_image(int(s), size, size)))
+            out.append(Image.fromarray(synthetic_image(int(s), int(h), int(w))))
     return out
 
 
@@ -54,7 +55,7 @@ def run_case(preset, tag=None):
 
     g = np.load(os.path.join(GOLD, f"{tag or preset + '_640'}.npz"))
     size = int(g["size"])
-    model = SpotterForObjectDetection(PRESETS[preset])
+    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)  # eager: read topk from _ws
     proc = SpotterImageProcessor(size={"height": size, "width": size})
     imgs = load_images(g)
     off = 0
@@ -94,6 +95,23 @@ def test_r101vd_matches_hf_goldens():
     run_case("r101vd")
 
 
+def test_r101vd_1280_mixed_resolution_matches_hf_goldens():
+    """C5: 720p / 1080p / 1200×717 sources resized on the GPU to 1280², per image and as one batch."""
+    model = run_case("r101vd", tag="r101vd_1280")
+    from spotter_amd import SpotterImageProcessor
+
+    g = np.load(os.path.join(GOLD, "r101vd_1280.npz"))
+    proc = SpotterImageProcessor(size={"height": 1280, "width": 1280})
+    imgs = load_images(g)
+    out = model(**proc(images=imgs))  # one mixed-size batch
+    dets = proc.post_process_object_detection(out, target_sizes=torch.tensor(g["target_sizes"]), threshold=0.5)
+    off = 0
+    for i, det in enumerate(dets):
+        n = int(g["det_counts"][i])
+        match_detections(det, g["det_scores"][off:off + n], g["det_labels"][off:off + n], g["det_boxes"][off:off + n])
+        off += n
+
+
 def test_batch_equals_single(tmp_path):
     """bs=3 in one engine call gives the same per-image outputs as three bs=1 calls."""
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
@@ -108,3 +126,22 @@ def test_batch_equals_single(tmp_path):
     for i, im in enumerate(imgs):
         o1 = model(**proc(images=im))
         np.testing.assert_allclose(o1.logits[0].cpu().numpy(), ob.logits[i].cpu().numpy(), rtol=0, atol=1e-4)
+
+
+def test_graph_replay_matches_eager():
+    """hipGraph-captured bs1 forward (spotter_amd/graph.py) equals the eager forward bit for bit,
+    and an eager call with a larger batch in between does not disturb the captured buffers."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.synthetic import synthetic_image
+
+    model = SpotterForObjectDetection(PRESETS["r18vd"], use_graphs=True)
+    proc = SpotterImageProcessor()
+    x = proc(images=synthetic_image(3))["pixel_values"]
+    e = model(pixel_values=x)          # eager (first sight of the shape)
+    g1 = model(pixel_values=x)         # captures + replays
+    model(**proc(images=[synthetic_image(4), synthetic_image(5), synthetic_image(6), synthetic_image(7),
+                         synthetic_image(8)]))  # eager, bigger workspace
+    g2 = model(pixel_values=x)         # replay
+    for o in (g1, g2):
+        assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)

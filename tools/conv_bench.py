@@ -21,6 +21,10 @@ SHAPES = [
     (1, 1, 268800, 256, 1536, 1, 1, None, False),    # value_all           2.7
     (32, 20, 20, 512, 2048, 1, 1, "relu", True),     # stage4 expand
     (1, 1, 9600, 256, 256, 1, 1, None, True),        # decoder linear
+    (64, 40, 40, 256, 256, 3, 1, "relu", False),     # 10: stage3 3x3 at 2x batch (tail test)
+    (128, 40, 40, 256, 256, 3, 1, "relu", False),    # 11: 4x batch
+    (32, 320, 320, 32, 32, 3, 1, "relu", False),     # 12: stem conv2 (N=32)
+    (32, 640, 640, 3, 32, 3, 2, "relu", False),      # 13: stem conv1 (Cin=3)
 ]
 
 

@@ -1,0 +1,70 @@
+"""p50/p95 latency of the /detect core at batch 1 (serve.py:96-117 minus HTTP/draw/JPEG):
+JPEG decode → processor → model → post_process → labels/boxes on the host.
+
+    python tools/latency.py [--iters 200] [--no-graph]
+"""
+import argparse
+import io
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from PIL import Image
+
+from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+from spotter_amd.config import PRESETS
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--preset", default="r101vd")
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    jpeg = open(os.path.join(root, "tests", "golden", "test_pic.jpg"), "rb").read()
+    model = SpotterForObjectDetection(PRESETS[a.preset], use_graphs=not a.no_graph)
+    proc = SpotterImageProcessor()
+
+    def detect():
+        with Image.open(io.BytesIO(jpeg)) as raw:
+            image = raw.convert("RGB")
+            inputs = proc(images=image, return_tensors="pt").to("cpu")
+            with torch.no_grad():
+                out = model(**inputs)
+            det = proc.post_process_object_detection(out, target_sizes=torch.tensor([[image.size[1], image.size[0]]]),
+                                                     threshold=0.5)[0]
+            labels = [model.config.id2label[int(l.item())] for l in det["labels"]]
+            boxes = det["boxes"].tolist()
+        return labels, boxes
+
+    for _ in range(5):
+        detect()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(a.iters):
+        t0 = time.perf_counter()
+        detect()
+        ts.append(time.perf_counter() - t0)
+    # GPU-only forward at bs1 (static input)
+    x = proc(images=Image.open(io.BytesIO(jpeg)).convert("RGB"))["pixel_values"]
+    fw = []
+    for _ in range(50):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        model(pixel_values=x)
+        torch.cuda.synchronize()
+        fw.append(time.perf_counter() - t0)
+    ts, fw = np.array(ts) * 1e3, np.array(fw) * 1e3
+    print(json.dumps({"metric": "p50 /detect core latency (bs1, 1200x717 JPEG)", "graphs": not a.no_graph,
+                      "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
+                      "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": a.iters,
+                      "preset": a.preset}))
+
+
+if __name__ == "__main__":
+    main()
