@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (v_mfma_f32_32x32x16_bf16), not the 2:1-sparse figure
 HBM_PEAK_GBS = 8000.0
 
 
@@ -39,6 +40,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="GEMM operand precision (bf16 = the separately reported variant, configs C3/C4)")
     ap.add_argument("--microbatches", type=int, default=1,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, +2%%,
                          but then per-launch durations overlap)")
@@ -157,7 +160,7 @@ def main():
 
     cfg = PRESETS[args.preset].replace(image_size=args.size)
     weights = generate(cfg, seed=0)
-    eng = Engine(cfg, weights, dev)
+    eng = Engine(cfg, weights, dev, precision=args.precision)
     eng.microbatches = args.microbatches
     B, S = args.batch, args.size
     imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
@@ -202,9 +205,12 @@ def main():
         ms, busy, fl, nl = rec.summary()
         per_launch_ms = ms / nl
         ach = fl / (busy * 1e-3) / 1e12
-        roof = {"bound": "mfma", "kernel": "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)",
-                "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+        peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        kname = ("conv_gemm_bf16_kernel (v_mfma_f32_32x32x16_bf16 implicit GEMM)" if args.precision == "bf16"
+                 else "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)")
+        roof = {"bound": "mfma", "kernel": kname,
+                "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": None,
                 "launches_per_step": nl // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
                 "gflop_per_step": round(fl / args.steps / 1e9, 2),
                 "conv_busy_ms_per_step": round(busy / args.steps, 3),
@@ -225,11 +231,12 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "images/sec RT-DETRv2-R101 640² bs32 (per GPU, replicas)" if args.preset == "r101vd"
-            else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B}",
+            "metric": ("images/sec RT-DETRv2-R101 640² bs32 (per GPU, replicas)"
+                       if (args.preset, S, B, args.precision) == ("r101vd", 640, 32, "fp32")
+                       else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B} {args.precision}"),
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic uint8 RGB images (seeded), synthetic deterministic weights",
             "config": {"workload": f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess",
                        "model": f"rtdetr_v2_{args.preset}", "global_batch": B * world, "image_size": S,

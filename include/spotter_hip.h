@@ -31,9 +31,12 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 1
+#define SP_ABI_VERSION 3
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
+/* GEMM operand precision: fp32 MFMA (exact fp32), or bf16 MFMA with fp32 accumulate
+ * (activations rounded to bf16 on load, weights from Wt_bf16). */
+enum sp_precision { SP_PREC_FP32 = 0, SP_PREC_BF16 = 1 };
 
 /* One uint8 RGB HWC image in device memory. */
 typedef struct {
@@ -52,6 +55,8 @@ typedef struct {
  * Output row m goes to C + (m / out_rows_per_group)*out_group_stride + (m % out_rows_per_group)*ldc
  * (out_rows_per_group = 0 means M, i.e. plain row-major with ldc).
  * res1/res2 rows use (m*ldr). Linear layers: N=1, H=1, W=rows, KH=KW=1.
+ * With a workspace, launches whose tile grid cannot fill the chip split K over the
+ * grid's z dimension and combine the partial sums (fixed order) before the epilogue.
  * Corresponds to nn.Conv2d + (Frozen)BatchNorm2d + activation (+ residual)
  * (RN:38-68, RN:225-231, M2:817-835) and nn.Linear (+ activation).
  */
@@ -70,6 +75,9 @@ typedef struct {
   const float* res2; int64_t ldr2;
   float* C; int64_t ldc;
   int32_t out_rows_per_group; int64_t out_group_stride;
+  float* workspace; int64_t workspace_elems; /* optional fp32 scratch enabling split-K (small M) */
+  int32_t precision;         /* sp_precision */
+  const uint16_t* Wt_bf16;   /* [Cout][K] bf16 weights (precision == SP_PREC_BF16) */
 } sp_conv_desc;
 
 /*

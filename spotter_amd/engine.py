@@ -40,18 +40,26 @@ def _t(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
 
 
-class ConvW:
-    __slots__ = ("w", "cin", "cout", "k", "scale", "shift")
+def bf16_bits(a: np.ndarray) -> np.ndarray:
+    """fp32 → bf16 bit patterns, round to nearest even (weights are finite)."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
 
-    def __init__(self, w, cin, cout, k, scale, shift):
+
+class ConvW:
+    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16")
+
+    def __init__(self, w, cin, cout, k, scale, shift, w16=None):
         self.w, self.cin, self.cout, self.k, self.scale, self.shift = w, cin, cout, k, scale, shift
+        self.w16 = w16
 
 
 class LinW:
-    __slots__ = ("w", "b", "k", "n")
+    __slots__ = ("w", "b", "k", "n", "w16")
 
-    def __init__(self, w, b, k, n):
+    def __init__(self, w, b, k, n, w16=None):
         self.w, self.b, self.k, self.n = w, b, k, n
+        self.w16 = w16
 
 
 def frozen_bn_affine(p, pre):
@@ -106,11 +114,15 @@ class Engine:
     """Owns the packed device weights and the per-shape workspaces of one GPU."""
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
-                 fold_repvgg: bool = True):
+                 fold_repvgg: bool = True, precision: str = "fp32"):
         from ._lib import lib
 
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
+        self.precision = precision
+        self._prec = 1 if precision == "bf16" else 0
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -128,18 +140,26 @@ class Engine:
         self.microbatches = 2
 
     # ------------------------------------------------------------------ weights
+    def _w16(self, wk: np.ndarray):
+        if self._prec == 0:
+            return None
+        return torch.from_numpy(bf16_bits(wk).view(np.int16)).to(self.dev)
+
+    def _mk_conv(self, wk, ci, co, k, sc, sh):
+        return ConvW(_t(wk, self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev), self._w16(wk))
+
     def _conv(self, p, conv_key, bn_pre, frozen):
         w = p[conv_key]
         co, ci, k, _ = w.shape
         sc, sh = (frozen_bn_affine if frozen else eval_bn_affine)(p, bn_pre)
-        return ConvW(_t(conv_khwc(w), self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev))
+        return self._mk_conv(conv_khwc(w), ci, co, k, sc, sh)
 
     def _lin(self, p, pre, *more):
         ws = [p[pre + ".weight"]] + [p[m + ".weight"] for m in more]
         bs = [p[pre + ".bias"]] + [p[m + ".bias"] for m in more]
-        w = np.concatenate(ws, 0)
+        w = np.ascontiguousarray(np.concatenate(ws, 0))
         b = np.concatenate(bs, 0)
-        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0])
+        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0], self._w16(w))
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -214,7 +234,8 @@ class Engine:
         c1 = self._conv(p, pre + ".conv1.conv.weight", pre + ".conv1.norm", False)
         c2 = self._conv(p, pre + ".conv2.conv.weight", pre + ".conv2.norm", False)
         c12 = ConvW(torch.cat([c1.w, c2.w], 0).contiguous(), c1.cin, c1.cout + c2.cout, 1,
-                    torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous())
+                    torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous(),
+                    None if c1.w16 is None else torch.cat([c1.w16, c2.w16], 0).contiguous())
         reps = []
         for b in range(3):
             q = f"{pre}.bottlenecks.{b}"
@@ -227,9 +248,9 @@ class Engine:
                 wf = (w3.astype(np.float64) * s1[:, None, None, None]).copy()
                 wf[:, :, 1, 1] += w1[:, :, 0, 0].astype(np.float64) * s2[:, None]
                 co, ci = w3.shape[:2]
-                reps.append(("fold", ConvW(_t(conv_khwc(wf.astype(np.float32)), self.dev), ci, co, 3,
-                                           _t(np.ones(co, np.float32), self.dev),
-                                           _t((b1.astype(np.float64) + b2).astype(np.float32), self.dev))))
+                reps.append(("fold", self._mk_conv(conv_khwc(wf.astype(np.float32)), ci, co, 3,
+                                                   np.ones(co, np.float32),
+                                                   (b1.astype(np.float64) + b2).astype(np.float32))))
             else:
                 reps.append((self._conv(p, q + ".conv1.conv.weight", q + ".conv1.norm", False),
                              self._conv(p, q + ".conv2.conv.weight", q + ".conv2.norm", False)))
@@ -256,14 +277,17 @@ class Engine:
         return c
 
     # ------------------------------------------------------------------ layers
+    SPLITK_ELEMS = 4 << 20  # 16 MB fp32 split-K scratch per context
+
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
-                          shift=cw.shift, act=act, res1=res1, res2=res2, **kw)
+                          shift=cw.shift, act=act, res1=res1, res2=res2,
+                          workspace=self._buf("splitk", self.SPLITK_ELEMS), wt16=cw.w16, **kw)
 
     def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None):
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                          row_scale=row_scale)
+                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), wt16=lw.w16)
 
     def backbone(self, px_nhwc: torch.Tensor, B, H, W):
         """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC)."""

@@ -58,7 +58,9 @@ def view(t: torch.Tensor, ld: int | None = None, off: int = 0) -> V:
 def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, k: int, stride: int,
            pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
-           rows_per_group: int = 0, group_stride: int = 0):
+           rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
+           wt16: torch.Tensor | None = None):
+    """wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path."""
     ho = (h + 2 * pad - k) // stride + 1
     wo = (w + 2 * pad - k) // stride + 1
     m = n * ho * wo
@@ -101,6 +103,15 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     d.ldc = out.ld
     d.out_rows_per_group = rows_per_group
     d.out_group_stride = group_stride
+    if wt16 is not None:
+        if wt16.numel() != cout * k * k * cin or wt16.dtype != torch.int16 or not wt16.is_contiguous():
+            raise ValueError("conv bf16 weight shape/dtype mismatch")
+        d.precision = 1
+        d.Wt_bf16 = wt16.data_ptr()
+    if workspace is not None:
+        assert workspace.dtype == torch.float32 and workspace.is_cuda
+        d.workspace = workspace.data_ptr()
+        d.workspace_elems = workspace.numel()
     if _conv_hook is None:
         call("sp_conv2d", C.byref(d), stream())
     else:
@@ -111,9 +122,9 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
            res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
-           scale=None):
+           scale=None, workspace=None, wt16=None):
     return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
-                  res2=res2, a2=a2, row_scale=row_scale)
+                  res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16)
 
 
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):

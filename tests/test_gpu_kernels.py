@@ -63,7 +63,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv2d_matches_oracle(dev, case):
+def test_conv2d_matches_oracle(dev, case, workspace=None):
     from spotter_amd import ops
     from spotter_amd.ops import view
 
@@ -83,7 +83,7 @@ def test_conv2d_matches_oracle(dev, case):
     wk = T(wt.transpose(0, 2, 3, 1).reshape(cout, -1), dev)
     ops.conv2d(view(T(x.reshape(-1), dev), cin), n, h, w, cin, wk, cout, k, st, pad, view(out, cout),
                scale=T(sc, dev), shift=T(sh, dev), act=act, res1=view(T(r1.reshape(-1), dev), cout),
-               res2=view(T(r2.reshape(-1), dev), cout))
+               res2=view(T(r2.reshape(-1), dev), cout), workspace=workspace)
     got = out.cpu().numpy().reshape(m, cout)
     # fp32 MFMA (exact fmaf chains) vs BLAS fp32: reassociation only
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
@@ -95,6 +95,50 @@ def test_conv2d_every_tile_config(dev, cfg, monkeypatch):
     monkeypatch.setenv("SP_CONV_CFG", cfg)
     for case in [(2, 11, 9, 64, 136, 3, 1, "silu"), (1, 7, 13, 96, 72, 1, 1, "relu"), (1, 9, 9, 3, 32, 3, 2, None)]:
         test_conv2d_matches_oracle(dev, case)
+
+
+@pytest.mark.parametrize("case", [(1, 5, 7, 256, 96, 3, 1, "relu"), (1, 1, 300, 1024, 256, 1, 1, None),
+                                  (1, 20, 20, 512, 130, 3, 1, "silu")])
+def test_conv2d_split_k(dev, case):
+    """Small-M / long-K launches split K over the grid when given a workspace (bs1 latency path)."""
+    ws = torch.empty(4 << 20, device=dev)
+    test_conv2d_matches_oracle(dev, case, workspace=ws)
+
+
+def _bf16(a):
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:7] + [(1, 5, 7, 256, 96, 3, 1, "relu")])
+@pytest.mark.parametrize("cfg", [None, "220", "120", "110"])
+def test_conv2d_bf16_matches_bf16_rounded_reference(dev, case, cfg, monkeypatch):
+    """bf16 MFMA path == exact math on bf16-rounded activations and weights (fp32 accumulate)."""
+    from spotter_amd import ops
+    from spotter_amd.engine import bf16_bits
+    from spotter_amd.ops import view
+
+    if cfg:
+        monkeypatch.setenv("SP_CONV_CFG", cfg)
+    n, h, w, cin, cout, k, st, act = case
+    rng = np.random.default_rng(hash(case) % 2**32 + 1)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32) * 0.1
+    pad = k // 2
+    ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+    m = n * ho * wo
+    r1 = rng.standard_normal((m, cout)).astype(np.float32)
+    ref = conv_ref(_bf16(x), _bf16(wt), st, pad, sc, sh, act, r1, None)
+    out = torch.empty(m * cout, device=dev)
+    wk = wt.transpose(0, 2, 3, 1).reshape(cout, -1)
+    w16 = torch.from_numpy(bf16_bits(wk).view(np.int16)).to(dev)
+    ws = torch.empty(4 << 20, device=dev)
+    ops.conv2d(view(T(x.reshape(-1), dev), cin), n, h, w, cin, T(wk, dev), cout, k, st, pad, view(out, cout),
+               scale=T(sc, dev), shift=T(sh, dev), act=act, res1=view(T(r1.reshape(-1), dev), cout), wt16=w16,
+               workspace=ws)
+    np.testing.assert_allclose(out.cpu().numpy().reshape(m, cout), ref, rtol=1e-3, atol=1e-3)
 
 
 def test_conv2d_strided_views_rowscale_a2_grouped(dev):

@@ -145,3 +145,14 @@ def test_graph_replay_matches_eager():
     g2 = model(pixel_values=x)         # replay
     for o in (g1, g2):
         assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)
+
+
+def test_bf16_variant_close_to_fp32_goldens():
+    """bf16 MFMA variant (reported separately): detections stay close to the fp32 reference."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from tools.bf16_delta import delta
+
+    d = delta("r18vd")
+    assert d["recall_vs_fp32"] >= 0.8, d
+    assert d["max_dscore"] <= 0.05, d
