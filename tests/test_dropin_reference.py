@@ -1,0 +1,145 @@
+"""CPU: the reference's own deployment module runs unchanged on top of spotter_amd.
+
+Loads apps/spotter/src/spotter/serve.py and schemas.py from /root/reference (this container only;
+skipped where the reference is absent, e.g. on the GPU box), applies exactly the two-line change
+documented in INTEGRATION.md §2 in memory, stubs the packages this image lacks (ray.serve,
+tenacity), and checks the AmenitiesDetector contract: construction (serve.py:66-72), the module-
+level `deployment = AmenitiesDetector.bind(model, processor)` (serve.py:199-205) with a picklable
+model, and the mocked `_process_single_image` flow of the reference's own unit tests
+(apps/spotter/tests/spotter/test_serve.py:80-148) driven through our processor/model types.
+"""
+import asyncio
+import importlib.util
+import os
+import pickle
+import sys
+import types
+from io import BytesIO
+from unittest.mock import AsyncMock, MagicMock, patch
+
+import pytest
+
+REF = "/root/reference/apps/spotter/src/spotter"
+pytestmark = pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+
+
+def _stub_modules():
+    ray = types.ModuleType("ray")
+    serve = types.ModuleType("ray.serve")
+
+    class _Deployment:
+        def __init__(self, cls):
+            self.func_or_class = cls
+
+        def bind(self, *args, **kwargs):
+            return ("bound", self.func_or_class, pickle.dumps((args, kwargs)))
+
+    serve.deployment = lambda cls: _Deployment(cls)
+    ray.serve = serve
+    ten = types.ModuleType("tenacity")
+
+    class AsyncRetrying:
+        def __init__(self, **kw):
+            pass
+
+        def __aiter__(self):
+            self._done = False
+            return self
+
+        async def __anext__(self):
+            if self._done:
+                raise StopAsyncIteration
+            self._done = True
+
+            class _A:
+                def __enter__(s):
+                    return s
+
+                def __exit__(s, *a):
+                    return False
+            return _A()
+
+    ten.AsyncRetrying = AsyncRetrying
+    ten.stop_after_attempt = lambda n: n
+    ten.wait_exponential = lambda **kw: kw
+    return {"ray": ray, "ray.serve": serve, "tenacity": ten}
+
+
+def _load_patched_serve(monkeypatch):
+    src = open(os.path.join(REF, "serve.py")).read()
+    old_model = "model = AutoModelForObjectDetection.from_pretrained(model_name).to(device)  # type: ignore"
+    old_proc = "processor = AutoImageProcessor.from_pretrained(model_name)"
+    assert old_model in src and old_proc in src, "reference serve.py changed; update INTEGRATION.md"
+    src = src.replace(old_model, "from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor\n"
+                                 "model = SpotterForObjectDetection.from_pretrained(model_name).to(device)")
+    src = src.replace(old_proc, "processor = SpotterImageProcessor.from_pretrained(model_name)")
+    for name, mod in _stub_modules().items():
+        monkeypatch.setitem(sys.modules, name, mod)
+    pkg = types.ModuleType("spotter")
+    pkg.__path__ = [REF]
+    monkeypatch.setitem(sys.modules, "spotter", pkg)
+    spec = importlib.util.spec_from_file_location("spotter.schemas", os.path.join(REF, "schemas.py"))
+    schemas = importlib.util.module_from_spec(spec)
+    monkeypatch.setitem(sys.modules, "spotter.schemas", schemas)
+    spec.loader.exec_module(schemas)
+    monkeypatch.setenv("MODEL_NAME", "PekingU/rtdetr_v2_r101vd")
+    mod = types.ModuleType("spotter.serve")
+    mod.__file__ = os.path.join(REF, "serve.py")
+    monkeypatch.setitem(sys.modules, "spotter.serve", mod)
+    exec(compile(src, mod.__file__, "exec"), mod.__dict__)
+    return mod, schemas
+
+
+def test_reference_deployment_module_binds_our_objects(monkeypatch):
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+
+    serve, _ = _load_patched_serve(monkeypatch)
+    assert isinstance(serve.model, SpotterForObjectDetection)
+    assert isinstance(serve.processor, SpotterImageProcessor)
+    kind, cls, blob = serve.deployment
+    assert kind == "bound" and cls.__name__ == "AmenitiesDetector"
+    (m, p), _ = pickle.loads(blob)  # what Ray ships to each replica: no device state inside
+    assert m._engine is None and m.config.id2label[62] == "tv"
+    det = cls(model=m, processor=p)  # serve.py:66-72 constructor check passes
+    assert det.processor is p
+
+
+def test_reference_process_single_image_flow_with_our_types(monkeypatch):
+    """serve.py:79-148 with our model/processor; kernels replaced by canned outputs (CPU only)."""
+    import torch
+
+    from spotter_amd import SpotterImageProcessor
+    from spotter_amd.model import SpotterDetectionOutput
+
+    serve, schemas = _load_patched_serve(monkeypatch)
+    cls = serve.deployment[1]
+    det = cls(model=serve.model, processor=serve.processor)
+    det.client = AsyncMock()
+    img_bytes = open(os.path.join(os.path.dirname(__file__), "golden", "test_pic.jpg"), "rb").read()
+    det._fetch_image_bytes = AsyncMock(return_value=img_bytes)
+    logits = torch.full((1, 300, 80), -9.0)
+    logits[0, 0, 62] = 3.0   # tv
+    logits[0, 1, 57] = 2.0   # couch
+    logits[0, 2, 65] = 1.0   # remote (not an amenity)
+    boxes = torch.tensor([[[0.5, 0.5, 0.2, 0.2]] * 300])
+
+    def fake_pp(outputs, threshold=0.5, target_sizes=None, use_focal_loss=True):
+        # the CPU oracle stands in for sp_postprocess (no GPU in this test)
+        from oracle.rtdetr_np import post_process
+        r = post_process(outputs.logits.numpy(), outputs.pred_boxes.numpy(), target_sizes.tolist(), threshold)[0]
+        return [{k: torch.from_numpy(v) for k, v in r.items()}]
+
+    from spotter_amd.processor import SpotterBatchFeature
+
+    def fake_proc(self, images=None, return_tensors="pt"):
+        assert images.mode == "RGB" and images.size == (1200, 717)
+        return SpotterBatchFeature(pixel_values=torch.zeros(1, 3, 640, 640))
+
+    with patch.object(SpotterImageProcessor, "__call__", fake_proc), \
+         patch.object(type(serve.model), "__call__", lambda self, **kw: SpotterDetectionOutput(logits, boxes)), \
+         patch.object(SpotterImageProcessor, "post_process_object_detection", lambda self, *a, **k: fake_pp(*a, **k)):
+        res = asyncio.run(det._process_single_image("local_test_image.jpg"))
+    assert isinstance(res, schemas.DetectionSuccessResult), getattr(res, "error", "")
+    assert [d.label for d in res.detections] == ["TV", "sofa"]
+    assert res.detections[0].box == pytest.approx([480.0, 286.8, 720.0, 430.2], abs=1e-3)
+    assert len(res.labeled_image_base64) > 500
