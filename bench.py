@@ -40,11 +40,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+    ap.add_argument("--stagger", type=int, default=1, help="block offset between micro-batch streams")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "bf16-all"],
                     help="GEMM operand precision (bf16 = the separately reported variant, configs C3/C4)")
     ap.add_argument("--microbatches", type=int, default=1,
-                    help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, +2%%,
-                         but then per-launch durations overlap)")
+                    help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
+                         "but then per-launch durations overlap)")
     return ap.parse_args()
 
 
@@ -162,6 +163,7 @@ def main():
     weights = generate(cfg, seed=0)
     eng = Engine(cfg, weights, dev, precision=args.precision)
     eng.microbatches = args.microbatches
+    eng.stagger = args.stagger
     B, S = args.batch, args.size
     imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
     imgs = [torch.from_numpy(im).to(dev) for im in imgs_host]  # resident in HBM
@@ -205,8 +207,9 @@ def main():
         ms, busy, fl, nl = rec.summary()
         per_launch_ms = ms / nl
         ach = fl / (busy * 1e-3) / 1e12
-        peak = BF16_MFMA_PEAK_TFLOPS if args.precision == "bf16" else FP32_MFMA_PEAK_TFLOPS
-        kname = ("conv_gemm_bf16_kernel (v_mfma_f32_32x32x16_bf16 implicit GEMM)" if args.precision == "bf16"
+        bf = args.precision.startswith("bf16")
+        peak = BF16_MFMA_PEAK_TFLOPS if bf else FP32_MFMA_PEAK_TFLOPS
+        kname = ("conv_gemm_bf16_kernel (v_mfma_f32_32x32x16_bf16 implicit GEMM; fp32 decoder GEMMs included)" if bf
                  else "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)")
         roof = {"bound": "mfma", "kernel": kname,
                 "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",

@@ -117,12 +117,14 @@ class Engine:
                  fold_repvgg: bool = True, precision: str = "fp32"):
         from ._lib import lib
 
-        if precision not in ("fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if precision not in ("fp32", "bf16", "bf16-all"):
+            raise ValueError("precision must be 'fp32', 'bf16' (backbone + encoder convs in bf16, the "
+                             "decoder / heads in fp32) or 'bf16-all'")
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
         self.precision = precision
-        self._prec = 1 if precision == "bf16" else 0
+        self._prec = 0 if precision == "fp32" else 1
+        self._prec_linear = 1 if precision == "bf16-all" else 0
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -138,6 +140,7 @@ class Engine:
         self._ctxs = {}
         self._outs = {}
         self.microbatches = 2
+        self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
     # ------------------------------------------------------------------ weights
     def _w16(self, wk: np.ndarray):
@@ -159,7 +162,8 @@ class Engine:
         bs = [p[pre + ".bias"]] + [p[m + ".bias"] for m in more]
         w = np.ascontiguousarray(np.concatenate(ws, 0))
         b = np.concatenate(bs, 0)
-        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0], self._w16(w))
+        w16 = self._w16(w) if self._prec_linear else None
+        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0], w16)
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -474,16 +478,31 @@ class Engine:
                 b0, b1 = bounds[i], bounds[i + 1]
                 jobs.append([ctx, self._run(pixel_values[b0:b1], out_logits[b0:b1], out_boxes[b0:b1])])
             saved = self._ws
+            # job i starts on the GPU only after job i-1 has issued `stagger` residual blocks
+            # (stream event), so the slices' GEMM tails do not line up.
+            steps = [0] * nmb
+            gate = [None] * nmb
             try:
-                while jobs:
-                    for job in list(jobs):
+                while any(j is not None for j in jobs):
+                    for ji, job in enumerate(jobs):
+                        if job is None:
+                            continue
                         ctx, g = job
+                        if ji > 0 and steps[ji] == 0:
+                            if gate[ji - 1] is None and jobs[ji - 1] is not None:
+                                continue
+                            if gate[ji - 1] is not None:
+                                ctx["stream"].wait_event(gate[ji - 1])
                         self._ws = ctx["ws"]
                         with torch.cuda.stream(ctx["stream"]):
                             try:
                                 next(g)
                             except StopIteration:
-                                jobs.remove(job)
+                                jobs[ji] = None
+                            steps[ji] += 1
+                            if steps[ji] == max(1, self.stagger) and gate[ji] is None:
+                                gate[ji] = torch.cuda.Event()
+                                gate[ji].record(ctx["stream"])
             finally:
                 self._ws = saved
             for i in range(nmb):

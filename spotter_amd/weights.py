@@ -145,17 +145,18 @@ def param_specs(cfg: SpotterConfig):
     nH, nL, nP = cfg.decoder_attention_heads, cfg.decoder_n_levels, cfg.decoder_n_points
     for j in range(cfg.decoder_layers):
         p = f"model.decoder.layers.{j}"
-        for n in ("k_proj", "v_proj", "q_proj", "o_proj"):
+        for n in ("k_proj", "v_proj", "q_proj"):
             _linear(sp, f"{p}.self_attn.{n}", D, D)
+        _linear(sp, f"{p}.self_attn.o_proj", D, D, role="resid_out")
         _ln(sp, f"{p}.self_attn_layer_norm", D)
         sp.append((f"{p}.encoder_attn.n_points_scale", (nL * nP,), ("misc", "npscale")))
         _linear(sp, f"{p}.encoder_attn.sampling_offsets", D, nH * nL * nP * 2, role="msda_off")
         _linear(sp, f"{p}.encoder_attn.attention_weights", D, nH * nL * nP, role="msda_aw")
         _linear(sp, f"{p}.encoder_attn.value_proj", D, D)
-        _linear(sp, f"{p}.encoder_attn.output_proj", D, D)
+        _linear(sp, f"{p}.encoder_attn.output_proj", D, D, role="resid_out")
         _ln(sp, f"{p}.encoder_attn_layer_norm", D)
         _linear(sp, f"{p}.mlp.fc1", D, cfg.decoder_ffn_dim)
-        _linear(sp, f"{p}.mlp.fc2", cfg.decoder_ffn_dim, D)
+        _linear(sp, f"{p}.mlp.fc2", cfg.decoder_ffn_dim, D, role="resid_out")
         _ln(sp, f"{p}.final_layer_norm", D)
     _linear(sp, "model.decoder.query_pos_head.layers.0", 4, 2 * D)
     _linear(sp, "model.decoder.query_pos_head.layers.1", 2 * D, D)
@@ -168,10 +169,16 @@ def param_specs(cfg: SpotterConfig):
     return sp
 
 
-# Logit bias of every class head: with unit-variance LayerNorm'd inputs and
-# 1/sqrt(fan_in) weights, logits ≈ N(CLS_BIAS, 1) so ~0.1% of the 24,000
-# (query, class) pairs clear the 0.5 threshold (SURVEY.md §7 "No real weights").
-CLS_BIAS = -3.5
+# Class heads: logits = CLS_GAIN·w·h + CLS_BIAS with unit-variance LayerNorm'd h, so a
+# few per mille of the 24,000 (query, class) pairs clear the 0.5 threshold with a
+# spread of scores up to ~0.95 (SURVEY.md §7 "No real weights").
+# RESID_GAIN scales the decoder's residual-branch outputs (self-attn o_proj, MSDA
+# output_proj, FFN fc2), the usual scaled-residual init: at 1.0 each decoder layer
+# pulls the 300 queries towards one vector (uniform random attention averages them),
+# so logits vary by class only and the detections are all-or-nothing per class.
+CLS_BIAS = -8.0
+CLS_GAIN = 3.0
+RESID_GAIN = 0.3
 
 
 def _msda_grid_bias(nH, nL, nP):
@@ -200,6 +207,10 @@ def generate(cfg: SpotterConfig, seed: int = 0) -> "OrderedDict[str, np.ndarray]
             w = w * np.float32(math.sqrt(2.0 / fan_in))
         elif kind == "bn_weight":
             lo, hi = (0.1, 0.3) if role == "resid_last" else (1.0, 1.6)
+            if key.startswith("model.encoder."):
+                # CCFM: RepVGG sums two branches and CSP adds two paths per block, so unit-gain
+                # BN would grow activations ~1000x over FPN+PAN and make the net chaotic.
+                lo, hi = (0.3, 0.6)
             w = rng.uniform(lo, hi, shape).astype(np.float32)
         elif kind == "bn_bias":
             w = (rng.standard_normal(shape) * 0.02).astype(np.float32)
@@ -211,6 +222,10 @@ def generate(cfg: SpotterConfig, seed: int = 0) -> "OrderedDict[str, np.ndarray]
             std = 1.0 / math.sqrt(shape[1])
             if role in ("box_last",):
                 std *= 0.05
+            elif role == "cls":
+                std *= CLS_GAIN
+            elif role == "resid_out":
+                std *= RESID_GAIN
             elif role == "msda_off":
                 std *= 0.02
             w = (rng.standard_normal(shape) * std).astype(np.float32)

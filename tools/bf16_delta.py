@@ -64,5 +64,7 @@ def delta(preset, tag=None, precision="bf16"):
 
 
 if __name__ == "__main__":
-    res = {p: delta(p) for p in ("r18vd", "r101vd")}
+    prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    res = {p: delta(p, precision=prec) for p in ("r18vd", "r101vd")}
+    res["precision"] = prec
     print(json.dumps({"metric": "bf16 variant detection delta vs HF fp32 goldens (synthetic weights)", **res}))
