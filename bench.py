@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (v_mfma_f32_32x32x16_bf16), not the 2:1-sparse figure
 HBM_PEAK_GBS = 8000.0
+BASELINE_METRIC = "images/sec RT-DETRv2-R101 640\u00b2 bs32 at 1/2/4/8 MI355X; p50 /detect latency"
 
 
 def parse():
@@ -39,6 +40,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--latency-iters", type=int, default=100,
+                    help="bs1 /detect core requests for the p50 latency half of the metric (0 = skip)")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
     ap.add_argument("--stagger", type=int, default=1, help="block offset between micro-batch streams")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "bf16-all"],
@@ -49,8 +52,36 @@ def parse():
     return ap.parse_args()
 
 
-class ConvEventRecorder:
-    """HIP events around every conv_gemm launch on the launch stream (torch's current stream)."""
+# kernel class -> (bound, peak, unit); peaks from MI355X_MICROARCH.md (dense, no sparsity)
+CLASS_BOUND = {
+    "conv": ("mfma", None, "TFLOP/s"),  # fp32 or bf16 MFMA peak by --precision
+    "attention": ("valu", 157.3, "TFLOP/s"),  # AIFI online-softmax attention, fp32 FMA on VALU
+    "msda": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "preprocess": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "topk": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "postprocess": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "layernorm": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "elementwise": ("hbm", HBM_PEAK_GBS, "GB/s"),
+}
+
+
+def union_ms(ivs):
+    union, cur_a, cur_b = 0.0, None, None
+    for a, b in sorted(ivs):
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                union += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    if cur_b is not None:
+        union += cur_b - cur_a
+    return union
+
+
+class KernelEventRecorder:
+    """HIP events around every kernel launch, recorded on the launch's own stream (the
+    engine makes each micro-batch stream torch's current stream before launching)."""
 
     def __init__(self, torch):
         self.torch = torch
@@ -58,43 +89,59 @@ class ConvEventRecorder:
         self.t0 = torch.cuda.Event(enable_timing=True)
         self.t0.record()
 
-    def __call__(self, launch, flops, shape=None):
+    def __call__(self, kind, launch, flops, nbytes, shape=None):
         t = self.torch
         e0 = t.cuda.Event(enable_timing=True)
         e1 = t.cuda.Event(enable_timing=True)
         e0.record()
         launch()
         e1.record()
-        self.recs.append((e0, e1, flops, shape))
+        self.recs.append((kind, e0, e1, flops, nbytes, shape))
 
-    def by_shape(self):
+    def by_shape(self, kind="conv"):
         agg = {}
-        for e0, e1, f, shp in self.recs:
+        for k, e0, e1, f, nb, shp in self.recs:
+            if k != kind:
+                continue
             a = agg.setdefault(str(shp), [0, 0.0, 0])
             a[0] += 1
             a[1] += e0.elapsed_time(e1)
             a[2] += f
-        rows = [{"shape(M,N,K,k,s)": k, "launches": v[0], "ms": round(v[1], 3),
+        rows = [{"shape": k, "launches": v[0], "ms": round(v[1], 3),
                  "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1)} for k, v in agg.items()]
         return sorted(rows, key=lambda r: -r["ms"])
 
-    def summary(self):
-        """(sum of launch durations, union of launch intervals, flops, launches) — launches of the
-        concurrent micro-batch streams overlap, so achieved TFLOP/s uses the busy-time union."""
-        ivs = sorted((self.t0.elapsed_time(r[0]), self.t0.elapsed_time(r[1])) for r in self.recs)
-        ms = sum(b - a for a, b in ivs)
-        union, cur_a, cur_b = 0.0, None, None
-        for a, b in ivs:
-            if cur_b is None or a > cur_b:
-                if cur_b is not None:
-                    union += cur_b - cur_a
-                cur_a, cur_b = a, b
-            else:
-                cur_b = max(cur_b, b)
-        if cur_b is not None:
-            union += cur_b - cur_a
-        fl = sum(r[2] for r in self.recs)
-        return ms, union, fl, len(self.recs)
+    def classes(self):
+        """kind -> dict(ms = sum of launch durations, busy = union of launch intervals, flops, bytes, n)."""
+        out = {}
+        for k, e0, e1, f, nb, _ in self.recs:
+            c = out.setdefault(k, {"ms": 0.0, "ivs": [], "flops": 0, "bytes": 0, "n": 0})
+            a, b = self.t0.elapsed_time(e0), self.t0.elapsed_time(e1)
+            c["ms"] += b - a
+            c["ivs"].append((a, b))
+            c["flops"] += f
+            c["bytes"] += nb
+            c["n"] += 1
+        for c in out.values():
+            c["busy"] = union_ms(c.pop("ivs"))
+        return out
+
+
+def load_traffic(args, avg_alg_bytes):
+    """HBM bytes per conv launch from the committed PMC passes (tools/pmc_bench.py), if they were
+    collected on this exact configuration; null otherwise."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.microbatches}"
+    e = t.get(key)
+    if not e:
+        return None, None
+    return e["conv_hbm_bytes_per_launch"], {"source": f"profiles/pmc_traffic.json[{key}]",
+                                            "ratio_to_algorithmic": round(e["conv_hbm_bytes_per_launch"]
+                                                                          / avg_alg_bytes, 3)}
 
 
 def cpu_baseline(cfg, weights, seconds):
@@ -185,8 +232,8 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    rec = None if args.no_events else ConvEventRecorder(torch)
-    ops.set_conv_hook(rec)
+    rec = None if args.no_events else KernelEventRecorder(torch)
+    ops.set_launch_hook(rec)
 
     barrier()
     torch.cuda.synchronize()
@@ -196,29 +243,47 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
-    ops.set_conv_hook(None)
+    ops.set_launch_hook(None)
     elapsed = t1 - t0
     elapsed = max_over_ranks(elapsed)
     n_img = world * B * args.steps
     value = n_img / elapsed
 
-    roof = None
+    roof, classes = None, None
     if rec is not None and rec.recs:
-        ms, busy, fl, nl = rec.summary()
-        per_launch_ms = ms / nl
-        ach = fl / (busy * 1e-3) / 1e12
+        cl = rec.classes()
         bf = args.precision.startswith("bf16")
-        peak = BF16_MFMA_PEAK_TFLOPS if bf else FP32_MFMA_PEAK_TFLOPS
+        conv_peak = BF16_MFMA_PEAK_TFLOPS if bf else FP32_MFMA_PEAK_TFLOPS
+        classes = {}
+        for kind, c in sorted(cl.items(), key=lambda kv: -kv[1]["ms"]):
+            bound, peak, unit = CLASS_BOUND[kind]
+            peak = peak or conv_peak
+            # concurrent micro-batch streams overlap launches of one class: use the busy-time union
+            work = c["bytes"] / 1e9 if unit == "GB/s" else c["flops"] / 1e12
+            ach = work / (c["busy"] * 1e-3)
+            classes[kind] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                             "frac": round(ach / peak, 4), "ms_per_step": round(c["busy"] / args.steps, 3),
+                             "launches_per_step": c["n"] // args.steps}
+        c = cl["conv"]
+        per_launch_ms = c["ms"] / c["n"]
+        ach = c["flops"] / (c["busy"] * 1e-3) / 1e12
+        alg_bytes = c["bytes"] / c["n"]
+        traffic, tnote = load_traffic(args, alg_bytes)
         kname = ("conv_gemm_bf16_kernel (v_mfma_f32_32x32x16_bf16 implicit GEMM; fp32 decoder GEMMs included)" if bf
                  else "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)")
         roof = {"bound": "mfma", "kernel": kname,
-                "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None,
-                "launches_per_step": nl // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
-                "gflop_per_step": round(fl / args.steps / 1e9, 2),
-                "conv_busy_ms_per_step": round(busy / args.steps, 3),
+                "achieved": round(ach, 2), "peak": conv_peak, "unit": "TFLOP/s",
+                "frac": round(ach / conv_peak, 4), "traffic": traffic,
+                "launches_per_step": c["n"] // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
+                "gflop_per_launch": round(c["flops"] / c["n"] / 1e9, 3),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2),
+                "conv_busy_ms_per_step": round(c["busy"] / args.steps, 3),
                 "note": "achieved = algorithmic conv/linear FLOPs / wall time with >=1 conv_gemm launch in flight "
-                        "(HIP events on the launch streams; micro-batch streams overlap)"}
+                        "(HIP events on the launch streams); traffic = HBM bytes per conv launch from PMC "
+                        "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
+        if tnote:
+            roof["traffic_source"] = tnote
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:
@@ -232,10 +297,18 @@ def main():
             cpu = {"value": None, "unit": "images/sec", "cores": None, "kind": "reference",
                    "sample": f"unavailable: {type(e).__name__}: {e}"}
 
+    lat = None
+    if rank == 0 and world == 1 and args.latency_iters > 0:
+        try:
+            from tools.latency import measure
+
+            lat = measure(args.preset, args.latency_iters, graphs=True)
+        except Exception as e:
+            lat = {"error": f"{type(e).__name__}: {e}"}
+
     if rank == 0:
         line = {
-            "metric": ("images/sec RT-DETRv2-R101 640² bs32 (per GPU, replicas)"
-                       if (args.preset, S, B, args.precision) == ("r101vd", 640, 32, "fp32")
+            "metric": (BASELINE_METRIC if (args.preset, S, B, args.precision) == ("r101vd", 640, 32, "fp32")
                        else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B} {args.precision}"),
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
@@ -244,7 +317,7 @@ def main():
             "config": {"workload": f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess",
                        "model": f"rtdetr_v2_{args.preset}", "global_batch": B * world, "image_size": S,
                        "parallelism": f"replicas x{world}"},
-            "roofline": roof, "cpu_baseline": cpu,
+            "roofline": roof, "kernel_classes": classes, "cpu_baseline": cpu, "latency": lat,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -15,13 +15,24 @@ from ._lib import SpConvDesc, SpImageU8, SpMsdaDesc, call
 
 ACT = {None: 0, "none": 0, "relu": 1, "silu": 2, "gelu": 3}
 
-_conv_hook = None
+_hook = None
 
 
-def set_conv_hook(hook):
-    """hook(launch: callable, flops: int, shape: (M, N, K, k, stride)) wraps every conv/linear launch (bench.py HIP-event timing)."""
-    global _conv_hook
-    _conv_hook = hook
+def set_launch_hook(hook):
+    """hook(kind, launch, flops, nbytes, shape) wraps every kernel launch (bench.py HIP-event timing).
+
+    kind is the kernel class ("conv", "msda", "attention", "preprocess", "topk", "layernorm",
+    "elementwise", "postprocess"); flops / nbytes are the launch's ALGORITHMIC work: useful
+    FLOPs and compulsory HBM bytes (every operand read once, every result written once)."""
+    global _hook
+    _hook = hook
+
+
+def _launch(kind: str, name: str, args, flops: int = 0, nbytes: int = 0, shape=None):
+    if _hook is None:
+        call(name, *args)
+    else:
+        _hook(kind, lambda: call(name, *args), flops, nbytes, shape)
 
 
 def stream() -> int:
@@ -112,11 +123,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
         d.workspace_elems = workspace.numel()
-    if _conv_hook is None:
-        call("sp_conv2d", C.byref(d), stream())
-    else:
-        _conv_hook(lambda: call("sp_conv2d", C.byref(d), stream()), 2 * m * cout * k * k * cin,
-                   (m, cout, k * k * cin, k, stride))
+    nbytes = 4 * (n * h * w * cin * (2 if a2 is not None else 1) + cout * k * k * cin + m * cout
+                  * (1 + (res1 is not None) + (res2 is not None)))
+    _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
+            (m, cout, k * k * cin, k, stride))
     return ho, wo
 
 
@@ -130,40 +140,47 @@ def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=No
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):
     n, c, h, w = x.shape
     assert y.numel() >= x.numel() and x.is_contiguous()
-    call("sp_nchw_to_nhwc", x.data_ptr(), y.data_ptr(), n, c, h, w, stream())
+    _launch("elementwise", "sp_nchw_to_nhwc", (x.data_ptr(), y.data_ptr(), n, c, h, w, stream()), 0,
+            8 * x.numel())
 
 
 def maxpool3x3s2(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
-    call("sp_maxpool3x3s2", x.data_ptr(), y.data_ptr(), n, h, w, c, stream())
+    _launch("elementwise", "sp_maxpool3x3s2", (x.data_ptr(), y.data_ptr(), n, h, w, c, stream()), 0,
+            4 * n * c * (h * w + ho * wo))
     return ho, wo
 
 
 def avgpool2x2_ceil(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
     ho, wo = (h + 1) // 2, (w + 1) // 2
     assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
-    call("sp_avgpool2x2_ceil", x.data_ptr(), y.data_ptr(), n, h, w, c, stream())
+    _launch("elementwise", "sp_avgpool2x2_ceil", (x.data_ptr(), y.data_ptr(), n, h, w, c, stream()), 0,
+            4 * n * c * (h * w + ho * wo))
     return ho, wo
 
 
 def upsample2x(x: V, y: V, n, h, w, c):
     xp = x.need(n * h * w, c, "upsample.x")
     yp = y.need(n * 4 * h * w, c, "upsample.y")
-    call("sp_upsample2x_nearest", xp, x.ld, yp, y.ld, n, h, w, c, stream())
+    _launch("elementwise", "sp_upsample2x_nearest", (xp, x.ld, yp, y.ld, n, h, w, c, stream()), 0,
+            4 * n * h * w * c * 5)
 
 
 def layernorm(x: V, gamma, beta, y: V, rows, d, eps=1e-5):
     xp = x.need(rows, d, "ln.x")
     yp = y.need(rows, d, "ln.y")
-    call("sp_layernorm", xp, x.ld, gamma.data_ptr(), beta.data_ptr(), yp, y.ld, rows, d, eps, stream())
+    _launch("layernorm", "sp_layernorm", (xp, x.ld, gamma.data_ptr(), beta.data_ptr(), yp, y.ld, rows, d, eps,
+                                           stream()), 8 * rows * d, 8 * rows * d)
 
 
 def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale):
     rows = batch * n
-    call("sp_attention", q.need(rows, heads * dh, "attn.q"), q.ld, k.need(rows, heads * dh, "attn.k"),
-         k.ld, v.need(rows, heads * dh, "attn.v"), v.ld, o.need(rows, heads * dh, "attn.o"), o.ld, batch,
-         n, heads, dh, scale, stream())
+    args = (q.need(rows, heads * dh, "attn.q"), q.ld, k.need(rows, heads * dh, "attn.k"), k.ld,
+            v.need(rows, heads * dh, "attn.v"), v.ld, o.need(rows, heads * dh, "attn.o"), o.ld, batch, n, heads,
+            dh, scale, stream())
+    _launch("attention", "sp_attention", args, 4 * batch * heads * n * n * dh, 16 * rows * heads * dh,
+            (batch, n, heads, dh))
 
 
 def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q, heads, head_dim,
@@ -183,7 +200,11 @@ def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q
     for i, ((h, w), s0) in enumerate(zip(shapes, starts)):
         d.level_h[i], d.level_w[i], d.level_start[i] = h, w, s0
     d.offset_scale = offset_scale
-    call("sp_msda", C.byref(d), stream())
+    # compulsory: the value maps once, offsets + weights + reference boxes per query, the output
+    nbytes = 4 * (B * S * heads * head_dim + B * Q * (heads * L * points * 3 + 4 + heads * head_dim))
+    # per sample: 4 bilinear taps (multiply-add) + the attention weight
+    flops = B * Q * heads * L * points * head_dim * 10
+    _launch("msda", "sp_msda", (C.byref(d), stream()), flops, nbytes, (B, S, Q, heads, head_dim, L, points))
 
 
 def topk_rows(x: V, rows, n, k, idx: torch.Tensor, vals: torch.Tensor | None = None, reduce_c=1,
@@ -192,26 +213,29 @@ def topk_rows(x: V, rows, n, k, idx: torch.Tensor, vals: torch.Tensor | None = N
     assert idx.dtype == torch.int32 and idx.numel() >= rows * k
     if vals is not None:
         assert vals.numel() >= rows * k
-    call("sp_topk_rows", xp, x.ld, rows, n, reduce_c, int(apply_sigmoid), k,
-         vals.data_ptr() if vals is not None else None, idx.data_ptr(), stream())
+    _launch("topk", "sp_topk_rows", (xp, x.ld, rows, n, reduce_c, int(apply_sigmoid), k,
+                                     vals.data_ptr() if vals is not None else None, idx.data_ptr(), stream()),
+            0, 4 * rows * (n * reduce_c + 2 * k), (rows, n, reduce_c, k))
 
 
 def gather_rows(src: V, src_rows, idx: torch.Tensor, k, batch, d, dst: V):
     sp_ = src.need(batch * src_rows, d, "gather.src")
     dp = dst.need(batch * k, d, "gather.dst")
-    call("sp_gather_rows", sp_, src.ld, src_rows, idx.data_ptr(), k, batch, d, dp, dst.ld, stream())
+    _launch("elementwise", "sp_gather_rows", (sp_, src.ld, src_rows, idx.data_ptr(), k, batch, d, dp, dst.ld,
+                                              stream()), 0, 4 * batch * k * (2 * d + 1))
 
 
 def ref_init(delta: V, anchors: torch.Tensor, idx: torch.Tensor, batch, k, ref: torch.Tensor):
     dp = delta.need(batch * k, 4, "ref_init.delta")
     assert ref.numel() >= batch * k * 4
-    call("sp_ref_init", dp, delta.ld, anchors.data_ptr(), idx.data_ptr(), batch, k, ref.data_ptr(), stream())
+    _launch("elementwise", "sp_ref_init", (dp, delta.ld, anchors.data_ptr(), idx.data_ptr(), batch, k,
+                                           ref.data_ptr(), stream()), 0, 4 * batch * k * 13)
 
 
 def box_refine(delta: V, ref: torch.Tensor, rows):
     dp = delta.need(rows, 4, "box_refine.delta")
     assert ref.numel() >= rows * 4
-    call("sp_box_refine", dp, delta.ld, ref.data_ptr(), rows, stream())
+    _launch("elementwise", "sp_box_refine", (dp, delta.ld, ref.data_ptr(), rows, stream()), 0, 4 * rows * 12)
 
 
 def preprocess_u8(images, out: torch.Tensor, out_h: int, out_w: int):
@@ -225,7 +249,9 @@ def preprocess_u8(images, out: torch.Tensor, out_h: int, out_w: int):
         arr[i].height, arr[i].width = im.shape[0], im.shape[1]
         arr[i].row_stride = im.shape[1] * 3
     assert out.numel() >= n * 3 * out_h * out_w and out.dtype == torch.float32
-    call("sp_preprocess_u8", arr, n, out_h, out_w, out.data_ptr(), stream())
+    nbytes = sum(int(im.numel()) for im in images) + 4 * n * 3 * out_h * out_w
+    _launch("preprocess", "sp_preprocess_u8", (arr, n, out_h, out_w, out.data_ptr(), stream()), 0, nbytes,
+            (n, out_h, out_w))
 
 
 def postprocess(logits: torch.Tensor, boxes: torch.Tensor, target_hw: torch.Tensor, k: int, threshold: float,
@@ -235,6 +261,6 @@ def postprocess(logits: torch.Tensor, boxes: torch.Tensor, target_hw: torch.Tens
     assert target_hw.dtype == torch.int32 and target_hw.numel() >= 2 * b
     assert scores.numel() >= b * k and labels.numel() >= b * k and labels.dtype == torch.int64
     assert boxes_xyxy.numel() >= b * k * 4 and counts.numel() >= b and work.numel() >= b * k
-    call("sp_postprocess", logits.data_ptr(), boxes.data_ptr(), target_hw.data_ptr(), b, q, c, k, threshold,
-         scores.data_ptr(), labels.data_ptr(), boxes_xyxy.data_ptr(), counts.data_ptr(), work.data_ptr(),
-         stream())
+    args = (logits.data_ptr(), boxes.data_ptr(), target_hw.data_ptr(), b, q, c, k, threshold, scores.data_ptr(),
+            labels.data_ptr(), boxes_xyxy.data_ptr(), counts.data_ptr(), work.data_ptr(), stream())
+    _launch("postprocess", "sp_postprocess", args, 0, 4 * b * (q * c + q * 4 + k * 7), (b, q, c, k))

@@ -19,15 +19,12 @@ from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
 from spotter_amd.config import PRESETS
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=200)
-    ap.add_argument("--preset", default="r101vd")
-    ap.add_argument("--no-graph", action="store_true")
-    a = ap.parse_args()
+def measure(preset="r101vd", iters=200, graphs=True, model=None):
+    """p50/p95 of the bs1 /detect core on the test fixture JPEG, plus the GPU-only forward p50."""
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    jpeg = open(os.path.join(root, "tests", "golden", "test_pic.jpg"), "rb").read()
-    model = SpotterForObjectDetection(PRESETS[a.preset], use_graphs=not a.no_graph)
+    with open(os.path.join(root, "tests", "golden", "test_pic.jpg"), "rb") as f:
+        jpeg = f.read()
+    model = model or SpotterForObjectDetection(PRESETS[preset], use_graphs=graphs)
     proc = SpotterImageProcessor()
 
     def detect():
@@ -46,12 +43,12 @@ def main():
         detect()
     torch.cuda.synchronize()
     ts = []
-    for _ in range(a.iters):
+    for _ in range(iters):
         t0 = time.perf_counter()
         detect()
         ts.append(time.perf_counter() - t0)
-    # GPU-only forward at bs1 (static input)
-    x = proc(images=Image.open(io.BytesIO(jpeg)).convert("RGB"))["pixel_values"]
+    with Image.open(io.BytesIO(jpeg)) as raw:
+        x = proc(images=raw.convert("RGB"))["pixel_values"]
     fw = []
     for _ in range(50):
         torch.cuda.synchronize()
@@ -60,10 +57,19 @@ def main():
         torch.cuda.synchronize()
         fw.append(time.perf_counter() - t0)
     ts, fw = np.array(ts) * 1e3, np.array(fw) * 1e3
-    print(json.dumps({"metric": "p50 /detect core latency (bs1, 1200x717 JPEG)", "graphs": not a.no_graph,
-                      "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
-                      "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": a.iters,
-                      "preset": a.preset}))
+    return {"metric": "p50 /detect core latency (bs1, 1200x717 JPEG: decode, preprocess, forward, "
+                      "post_process, labels/boxes to host)", "graphs": graphs,
+            "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
+            "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": iters, "preset": preset}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--preset", default="r101vd")
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args()
+    print(json.dumps(measure(a.preset, a.iters, not a.no_graph)))
 
 
 if __name__ == "__main__":
