@@ -177,7 +177,14 @@ def cpu_baseline(cfg, weights, seconds):
         if time.perf_counter() - t0 >= seconds and n >= 3:
             break
     dt = time.perf_counter() - t0
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
     return {"value": n / dt, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "reference",
+            "cpu_model": cpu_model,
             "sample": f"{n} images bs=1 {cfg.image_size}x{cfg.image_size} through HF transformers "
                       f"RTDetrImageProcessorPil+RTDetrV2ForObjectDetection(fp32, synthetic {cfg.name} weights)"
                       f"+post_process_object_detection on {torch.get_num_threads()} host threads, {dt:.1f}s"}

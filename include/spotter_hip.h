@@ -102,6 +102,9 @@ typedef struct {
 int sp_abi_version(void);
 const char* sp_last_error(void);
 int sp_device_init(int device);
+/* Frees the cached resample coefficient tables (the only state kept across
+ * calls). Safe to call at any time; the next sp_preprocess_u8 rebuilds what it needs. */
+int sp_shutdown(void);
 
 /* RTDetrImageProcessorPil resize (PIL BILINEAR, bit-exact) + rescale 1/255 + HWC→CHW
  * (IPP:451-462, IT:118-122, IT:367). out: [n, 3, out_h, out_w] fp32. */

@@ -4,7 +4,7 @@ Runs the reference's own call pattern (serve.py:98-109): HF
 `RTDetrImageProcessorPil` → `RTDetrV2ForObjectDetection` (built by
 oracle/hf_ref.py with spotter_amd.weights.generate(cfg, seed=0)) →
 `post_process_object_detection(threshold=0.5, target_sizes=[(h, w)])`, on
-seeded synthetic images (spotter_amd.synthetic) plus the reference's own test
+seeded synthetic images and a flat mid-gray frame (spotter_amd.synthetic) plus the reference's own test
 fixture image (apps/spotter/tests/spotter/test_data/test_pic.jpg, copied to
 tests/golden/test_pic.jpg as data). Only inputs' seeds, output tensors and
 digests are stored — no reference source.
@@ -64,13 +64,13 @@ def make_preprocess():
                         seeds=np.array(rec["seeds"]), digests=np.array(rec["digests"]))
 
 
-def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=None, src_sizes=None):
+def make_model(preset: str, size: int = 640, seeds=(0, 1, -2), with_pic=True, tag=None, src_sizes=None):
     import torch
     from PIL import Image
 
     from oracle.hf_ref import build_hf_model, build_hf_processor
     from spotter_amd.config import PRESETS
-    from spotter_amd.synthetic import synthetic_image
+    from spotter_amd.synthetic import golden_source
     from spotter_amd.weights import generate
 
     torch.manual_seed(0)
@@ -80,7 +80,8 @@ def make_model(preset: str, size: int = 640, seeds=(0, 1), with_pic=True, tag=No
     pp = build_hf_processor()
     pp.size = {"height": size, "width": size}
     src_sizes = list(src_sizes or [(size, size)] * len(seeds))
-    imgs = [synthetic_image(s, h, w) for s, (h, w) in zip(seeds, src_sizes)]
+    pic = os.path.join(GOLD, "test_pic.jpg")
+    imgs = [golden_source(s, h, w, pic) for s, (h, w) in zip(seeds, src_sizes)]
     if with_pic:
         imgs.append(load_test_pic())
         src_sizes.append(imgs[-1].shape[:2])
@@ -129,8 +130,9 @@ def main(argv):
         make_model("r101vd")
     if "r101vd_1280" in what:
         # C5: mixed-resolution stream resized on the GPU to 1280²
-        make_model("r101vd", size=1280, seeds=(0, 1), with_pic=True, tag="r101vd_1280",
-                   src_sizes=[(720, 1280), (1080, 1920)])
+        # (D1.3 stream sizes; the 717x1200 one is the fixture picture itself)
+        make_model("r101vd", size=1280, seeds=(0, 1, 2, 3, 4), with_pic=True, tag="r101vd_1280",
+                   src_sizes=[(480, 640), (720, 1280), (1080, 1920), (1280, 1280), (2160, 3840)])
 
 
 if __name__ == "__main__":

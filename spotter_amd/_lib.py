@@ -61,6 +61,7 @@ _SIGS = {
     "sp_abi_version": (i32, []),
     "sp_last_error": (C.c_char_p, []),
     "sp_device_init": (i32, [i32]),
+    "sp_shutdown": (i32, []),
     "sp_preprocess_u8": (i32, [C.POINTER(SpImageU8), i32, i32, i32, vp, vp]),
     "sp_conv2d": (i32, [C.POINTER(SpConvDesc), vp]),
     "sp_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, vp]),

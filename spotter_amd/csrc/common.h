@@ -13,6 +13,7 @@ namespace sp {
 
 void set_error(const char* fmt, ...);
 void clear_error();
+void free_coeff_cache();
 
 // Returns 0 after a successful async launch, else the hipError_t (and records it).
 inline int check_launch(const char* what) {

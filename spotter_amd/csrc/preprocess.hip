@@ -34,6 +34,7 @@ struct Coeffs {
 
 std::mutex g_mu;
 std::map<std::pair<int, int>, Coeffs> g_cache;
+const Coeffs c_failed;
 
 // Resample.c precompute_coeffs + normalize_coeffs_8bpc for the bilinear filter.
 void precompute(int in_size, int out_size, Coeffs& c) {
@@ -69,10 +70,15 @@ void precompute(int in_size, int out_size, Coeffs& c) {
   }
   c.ksize = ksize;
   c.h_bounds = bounds;
-  hipMalloc(&c.d_bounds, bounds.size() * sizeof(int));
-  hipMalloc(&c.d_k, kk.size() * sizeof(int));
-  hipMemcpy(c.d_bounds, bounds.data(), bounds.size() * sizeof(int), hipMemcpyHostToDevice);
-  hipMemcpy(c.d_k, kk.data(), kk.size() * sizeof(int), hipMemcpyHostToDevice);
+  if (hipMalloc(&c.d_bounds, bounds.size() * sizeof(int)) != hipSuccess ||
+      hipMalloc(&c.d_k, kk.size() * sizeof(int)) != hipSuccess ||
+      hipMemcpy(c.d_bounds, bounds.data(), bounds.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c.d_k, kk.data(), kk.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+    if (c.d_bounds) hipFree(c.d_bounds);
+    if (c.d_k) hipFree(c.d_k);
+    c.d_bounds = nullptr;
+    c.d_k = nullptr;
+  }
 }
 
 const Coeffs* get_coeffs(int in_size, int out_size) {
@@ -82,6 +88,7 @@ const Coeffs* get_coeffs(int in_size, int out_size) {
   if (it != g_cache.end()) return &it->second;
   Coeffs c;
   precompute(in_size, out_size, c);
+  if (!c.d_k) return &c_failed;  // not cached: the next call retries the upload
   return &(g_cache[key] = std::move(c));
 }
 
@@ -180,6 +187,16 @@ int band_rows(const Coeffs& v, int out_h, int row_bytes, int* ntiles) {
 }
 
 }  // namespace
+
+// sp_shutdown: release the device coefficient tables (the only state the ABI keeps).
+void free_coeff_cache() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& kv : g_cache) {
+    hipFree(kv.second.d_bounds);
+    hipFree(kv.second.d_k);
+  }
+  g_cache.clear();
+}
 }  // namespace sp
 
 extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int out_w, float* out,

@@ -39,3 +39,8 @@ extern "C" int sp_device_init(int device) {
   }
   return 0;
 }
+
+extern "C" int sp_shutdown(void) {
+  sp::free_coeff_cache();
+  return 0;
+}

@@ -42,5 +42,21 @@ def synthetic_image(seed: int, h: int = 640, w: int = 640, flat: bool = False) -
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
+TEST_PIC_SEED = -1  # the reference's own fixture, tests/golden/test_pic.jpg
+FLAT_GRAY_SEED = -2  # a constant mid-gray frame (SURVEY.md §8 D1.3 parity set)
+
+
+def golden_source(seed: int, h: int, w: int, pic_path: str) -> np.ndarray:
+    """The uint8 HWC source image a golden record names by (seed, h, w)."""
+    if seed == TEST_PIC_SEED:
+        from PIL import Image
+
+        with Image.open(pic_path) as im:
+            return np.asarray(im.convert("RGB"))
+    if seed == FLAT_GRAY_SEED:
+        return np.full((h, w, 3), 128, dtype=np.uint8)
+    return synthetic_image(seed, h, w)
+
+
 def synthetic_batch(n: int, h: int = 640, w: int = 640, seed0: int = 1234) -> np.ndarray:
     return np.stack([synthetic_image(seed0 + i, h, w) for i in range(n)])

@@ -62,7 +62,7 @@ def test_numpy_oracle_matches_hf_goldens(preset):
     from oracle import rtdetr_np
     from oracle.pil_resize import preprocess
     from spotter_amd.config import PRESETS
-    from spotter_amd.synthetic import synthetic_image
+    from spotter_amd.synthetic import golden_source
     from spotter_amd.weights import generate
 
     g = np.load(os.path.join(GOLD, f"{preset}_640.npz"))
@@ -71,12 +71,7 @@ def test_numpy_oracle_matches_hf_goldens(preset):
     off = 0
     n_img = 2 if preset == "r101vd" else len(g["seeds"])
     for i in range(n_img):
-        s = int(g["seeds"][i])
-        if s < 0:
-            with Image.open(os.path.join(GOLD, "test_pic.jpg")) as im:
-                img = np.asarray(im.convert("RGB"))
-        else:
-            img = synthetic_image(s, 640, 640)
+        img = golden_source(int(g["seeds"][i]), 640, 640, os.path.join(GOLD, "test_pic.jpg"))
         st = rtdetr_np.forward(preprocess(img)[None], w, cfg)
         common = set(st["enc_topk_ind"][0].tolist()) & set(g["enc_topk_ind"][i].tolist())
         assert len(common) >= 298

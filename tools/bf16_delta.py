@@ -36,6 +36,7 @@ def delta(preset, tag=None, precision="bf16"):
     proc = SpotterImageProcessor(size={"height": size, "width": size})
     off = 0
     tot = dict(expected=0, matched=0, extra=0, max_dscore=0.0, max_dbox_px=0.0)
+    ds = []
     for i, img in enumerate(load_images(g)):
         out = model(**proc(images=img))
         th, tw = g["target_sizes"][i]
@@ -55,11 +56,14 @@ def delta(preset, tag=None, precision="bf16"):
             if bi >= 0 and best >= 0.5:
                 used.add(bi)
                 tot["matched"] += 1
-                tot["max_dscore"] = max(tot["max_dscore"], abs(float(det["scores"][bi]) - float(s)))
+                ds.append(abs(float(det["scores"][bi]) - float(s)))
+                tot["max_dscore"] = max(tot["max_dscore"], ds[-1])
                 tot["max_dbox_px"] = max(tot["max_dbox_px"], float(np.abs(det["boxes"][bi].numpy() - b).max()))
         tot["expected"] += n
         tot["extra"] += len(det["scores"]) - len(used)
     tot["recall_vs_fp32"] = tot["matched"] / max(1, tot["expected"])
+    tot["p50_dscore"] = float(np.percentile(ds, 50)) if ds else 0.0
+    tot["p95_dscore"] = float(np.percentile(ds, 95)) if ds else 0.0
     return tot
 
 
