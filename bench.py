@@ -44,8 +44,9 @@ def parse():
                     help="bs1 /detect core requests for the p50 latency half of the metric (0 = skip)")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
     ap.add_argument("--stagger", type=int, default=1, help="block offset between micro-batch streams")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "bf16-all"],
-                    help="GEMM operand precision (bf16 = the separately reported variant, configs C3/C4)")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-mfma", "bf16", "bf16-all"],
+                    help="GEMM operand precision: fp32 = fp32-accurate 3-way bf16 split GEMMs (SP_PREC_F32X3), "
+                         "fp32-mfma = v_mfma_f32_32x32x2_f32 GEMMs; bf16 = the separately reported variant (C3/C4)")
     ap.add_argument("--microbatches", type=int, default=1,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")

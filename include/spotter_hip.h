@@ -31,12 +31,21 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 3
+#define SP_ABI_VERSION 4
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
-/* GEMM operand precision: fp32 MFMA (exact fp32), or bf16 MFMA with fp32 accumulate
- * (activations rounded to bf16 on load, weights from Wt_bf16). */
-enum sp_precision { SP_PREC_FP32 = 0, SP_PREC_BF16 = 1 };
+/* GEMM operand precision:
+ *  SP_PREC_FP32  fp32 MFMA (v_mfma_f32_32x32x2_f32: an exact fp32 fmaf chain);
+ *  SP_PREC_BF16  bf16 MFMA with fp32 accumulate (activations rounded RNE to bf16 on load,
+ *                weights from Wt_bf16) — the separately reported bf16 variant;
+ *  SP_PREC_F32X3 fp32 operands as 3-way bf16 splits x = hi + mid + lo (24 significand bits,
+ *                exact for normal fp32), products hi·hi + hi·mid + mid·hi + hi·lo + lo·hi +
+ *                mid·mid on bf16 MFMA with fp32 accumulate; the dropped terms sum to <= 2^-24
+ *                of |a·b| (one fp32 rounding), so the result is fp32-accurate (checked against
+ *                fp64 next to the fp32 MFMA path in tests/test_gpu_kernels.py).
+ *                Weights from Wt_bf16 as three planes [3][Cout][K] (plane stride
+ *                wt_plane_stride); activations are split while staging. */
+enum sp_precision { SP_PREC_FP32 = 0, SP_PREC_BF16 = 1, SP_PREC_F32X3 = 2 };
 
 /* One uint8 RGB HWC image in device memory. */
 typedef struct {
@@ -77,7 +86,8 @@ typedef struct {
   int32_t out_rows_per_group; int64_t out_group_stride;
   float* workspace; int64_t workspace_elems; /* optional fp32 scratch enabling split-K (small M) */
   int32_t precision;         /* sp_precision */
-  const uint16_t* Wt_bf16;   /* [Cout][K] bf16 weights (precision == SP_PREC_BF16) */
+  const uint16_t* Wt_bf16;   /* [Cout][K] bf16 weights (SP_PREC_BF16), [3][Cout][K] (SP_PREC_F32X3) */
+  int64_t wt_plane_stride;   /* elements between the hi / mid / lo planes (SP_PREC_F32X3) */
 } sp_conv_desc;
 
 /*

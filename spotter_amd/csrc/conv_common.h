@@ -1,0 +1,188 @@
+// Shared pieces of the implicit-GEMM conv kernels (conv_gemm.hip: fp32 MFMA;
+// conv_mfma16.hip: bf16 / 3-way-split MFMA): launch arguments and the fused epilogue.
+#pragma once
+
+#include "common.h"
+
+namespace sp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float act_apply(float v, int act) {
+  if (act == SP_ACT_RELU) return fmaxf(v, 0.0f);
+  if (act == SP_ACT_SILU) return v / (1.0f + expf(-v));
+  if (act == SP_ACT_GELU) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
+  return v;
+}
+
+struct ConvArgs {
+  sp_conv_desc d;
+  int64_t M;
+  int32_t K;
+  int32_t HoWo;
+  int32_t fast;     // Cin % 32 == 0 and 16-byte aligned operands
+  int32_t vec_epi;  // 16-byte aligned C/res/scale/shift rows → float4 epilogue
+  int32_t splits;   // split-K factor (>1: raw partial sums to `partial`, epilogue in splitk_reduce)
+  int32_t ldp;      // row stride of a partial slab (Cout rounded up to 4)
+  float* partial;   // [splits][M][ldp]
+};
+
+// Output row pointer: plain row-major (out_rows_per_group == 0) or grouped rows.
+__device__ __forceinline__ float* out_row(const sp_conv_desc& d, int64_t m) {
+  if (d.out_rows_per_group <= 0) return d.C + m * d.ldc;
+  const int64_t g = m / d.out_rows_per_group;
+  return d.C + g * d.out_group_stride + (m - g * d.out_rows_per_group) * d.ldc;
+}
+
+// The fused epilogue on four consecutive output channels n..n+3 of row m (p.vec_epi, n+3 < Cout),
+// with the res1 row segment already loaded (r1; ignored when d.res1 is null).
+__device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n, float4 v, float4 r1) {
+  const sp_conv_desc& d = p.d;
+  if (d.row_scale) {
+    const float rs = d.row_scale[m % d.row_period];
+    v.x *= rs; v.y *= rs; v.z *= rs; v.w *= rs;
+  }
+  const float4 sc = d.scale ? *reinterpret_cast<const float4*>(d.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y);
+  v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
+  if (d.res1) {
+    v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
+  }
+  v.x = act_apply(v.x, d.act); v.y = act_apply(v.y, d.act);
+  v.z = act_apply(v.z, d.act); v.w = act_apply(v.w, d.act);
+  if (d.res2) {
+    const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  *reinterpret_cast<float4*>(out_row(d, m) + n) = v;
+}
+
+// The fused epilogue on four consecutive output channels n..n+3 of row m.
+__device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int n, float4 v) {
+  const sp_conv_desc& d = p.d;
+  if (p.vec_epi && n + 3 < d.Cout) {
+    const float4 r1 = d.res1 ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    epilogue_vec(p, m, n, v, r1);
+  } else {
+    float* crow = out_row(d, m);
+    float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int nn = n + u;
+      if (nn >= d.Cout) break;
+      float x = e[u];
+      if (d.row_scale) x *= d.row_scale[m % d.row_period];
+      x = fmaf(x, d.scale ? d.scale[nn] : 1.0f, d.shift ? d.shift[nn] : 0.0f);
+      if (d.res1) x += d.res1[m * d.ldr1 + nn];
+      x = act_apply(x, d.act);
+      if (d.res2) x += d.res2[m * d.ldr2 + nn];
+      crow[nn] = x;
+    }
+  }
+}
+
+// Accumulator band i of a wave (TN 32x32 MFMA tiles, v_mfma_f32_32x32x*: lane (r, h) holds
+// rows (q&3) + 8(q>>2) + 4h, column r) → the wave's private LDS slab → fused epilogue on
+// float4s of one output row (or raw partial sums for split-K).
+template <int TN>
+__device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, const f32x16* accrow,
+                                              int64_t mb, int nb, int lane) {
+  constexpr int WN = TN * 32;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) slab[((q & 3) + 8 * (q >> 2) + 4 * h) * WN + j * 32 + r] = accrow[j][q];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int t = 0; t < (32 * WN / 4) / 64; ++t) {
+    const int c = lane + 64 * t;
+    const int row = c / (WN / 4);
+    const int col = (c - row * (WN / 4)) * 4;
+    const int64_t m = mb + row;
+    const int n = nb + col;
+    if (m >= p.M || n >= p.d.Cout) continue;
+    float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
+    if (p.splits > 1) {
+      *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+    } else {
+      epilogue_store(p, m, n, v);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The TM accumulator bands of a wave → its LDS region (NB bands of 32 × 32TN floats at a time),
+// then the fused epilogue on float4s of one output row, with the res1 loads of G consecutive
+// tasks issued before their stores so the residual fetch latency overlaps. NB = TM when the
+// region fits in the operand stages' LDS, else 1 (band by band).
+template <int TM, int TN, int NB>
+__device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, f32x16 (*acc)[TN],
+                                              int64_t mb, int nb, int lane) {
+  static_assert(TM % NB == 0, "bands per round must divide TM");
+  constexpr int WN = TN * 32;
+  constexpr int PER = NB * (32 * WN / 4) / 64;  // float4 tasks per lane per round
+  constexpr int G = PER < 4 ? PER : 4;
+  static_assert(PER % G == 0, "task groups");
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const sp_conv_desc& d = p.d;
+  const bool fastv = p.vec_epi && p.splits == 1;
+#pragma unroll
+  for (int i0 = 0; i0 < TM; i0 += NB) {
+    if (i0) __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          region[(i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h) * WN + j * 32 + r] = acc[i0 + i][j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    const int64_t mr = mb + i0 * 32;
+    for (int t0 = 0; t0 < PER; t0 += G) {
+      float4 r1[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int cidx = lane + 64 * (t0 + u);
+        const int row = cidx / (WN / 4);
+        const int col = (cidx - row * (WN / 4)) * 4;
+        const int64_t m = mr + row;
+        const int n = nb + col;
+        r1[u] = (fastv && d.res1 && m < p.M && n < d.Cout)
+                    ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int cidx = lane + 64 * (t0 + u);
+        const int row = cidx / (WN / 4);
+        const int col = (cidx - row * (WN / 4)) * 4;
+        const int64_t m = mr + row;
+        const int n = nb + col;
+        if (m >= p.M || n >= d.Cout) continue;
+        const float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
+        if (p.splits > 1) {
+          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+        } else if (fastv) {
+          epilogue_vec(p, m, n, v, r1[u]);
+        } else {
+          epilogue_store(p, m, n, v);
+        }
+      }
+    }
+  }
+}
+
+// conv_mfma16.hip: bf16-operand MFMA GEMM (planes = 1: bf16; planes = 3: fp32 via a 3-way bf16
+// split). cfg < 0 picks the tile by shape. Returns 0 or the launch error.
+int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+// Split-K combine kernel launch (conv_gemm.hip).
+int launch_splitk_reduce(const ConvArgs& a, hipStream_t s);
+
+}  // namespace sp

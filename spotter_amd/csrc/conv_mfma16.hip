@@ -1,0 +1,620 @@
+// Implicit-GEMM convolution / linear layer on bf16-operand MFMA (v_mfma_f32_32x32x16_bf16,
+// fp32 accumulate) for gfx950. Two operand modes share one kernel body:
+//
+//   PL = 1  bf16: activations rounded RNE to bf16 while staging, weights pre-rounded bf16
+//           (sp_precision SP_PREC_BF16, the separately reported bf16 variant);
+//   PL = 3  fp32 via a 3-way split (SP_PREC_F32X3): each fp32 operand x = hi + mid + lo with
+//           hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid) (both differences are exact
+//           in fp32), so the three planes hold all 24 significand bits. Per 16-deep k step the
+//           wave issues the six products down to the 2^-17 |a b| scale:
+//             lo·hi, hi·lo, mid·mid, mid·hi, hi·mid, hi·hi   (smallest first)
+//           With round-to-nearest |mid| <= 2^-8 |x| and |lo| <= 2^-17 |x|, so the dropped mid·lo,
+//           lo·mid, lo·lo terms sum to <= 2^-24 |a b| — one fp32 rounding of the product — and
+//           every bf16×bf16 product is exact in the fp32 accumulator. The MFMA
+//           accumulator is rounded 6 times per 16 k here versus 16 times for the fp32 MFMA
+//           (v_mfma_f32_32x32x2_f32 ≡ an fmaf chain), so the result is fp32-accurate while the
+//           matrix core runs 6 × 32 = 192 cycles per 32×32×16 block instead of 8 × 64 = 512.
+//
+// Same GEMM contract and fused epilogue as conv_gemm.hip (conv_common.h): A gathered on the fly
+// from NHWC activations (implicit im2col), W as [Cout][K] bf16 planes (k contiguous).
+//
+// Tiling: WM×WN waves per workgroup, each wave a (32·TM)×(32·TN) patch of 32×32 accumulators;
+// BK = 32 k per LDS stage (two 16-deep MFMA steps). Operand tiles are staged global → registers
+// (fp32 A split into planes on the way) → LDS, double-buffered with one barrier per k-tile.
+// LDS planes are [rows][32 bf16] = four 16-byte chunks per row; chunk c of row r lives at
+// r·4 + (c ^ ((r >> 2) & 3)), which makes the 16-lane groups of every ds_read_b128 fragment
+// read (lanes r = 0..31 of one chunk) hit 16 distinct bank slots, and keeps the 8-lane groups
+// of the ds_write_b128 staging stores conflict-free.
+// The 1-D grid is remapped XCD-aware (MI355X dispatches consecutive workgroups round-robin over
+// the 8 XCDs): each XCD receives a contiguous run of output tiles, N fastest, so workgroups that
+// share an A row-panel share one L2.
+#include <cstdlib>
+
+#include "conv_common.h"
+
+namespace sp {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int KT = 32;  // k per LDS stage
+
+__device__ __forceinline__ int sw16(int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); }
+
+// 8 fp32 → PL bf16 planes (RNE). PL = 3: exact residual chain hi / mid / lo.
+template <int PL>
+__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8* out) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  bf16x8 h, m, l;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    h[j] = (__bf16)v[j];
+    if constexpr (PL == 3) {
+      const float r1 = v[j] - (float)h[j];
+      m[j] = (__bf16)r1;
+      const float r2 = r1 - (float)m[j];
+      l[j] = (__bf16)r2;
+    }
+  }
+  out[0] = h;
+  if constexpr (PL == 3) {
+    out[1] = m;
+    out[2] = l;
+  }
+}
+
+template <int PL>
+__device__ __forceinline__ f32x16 mfma_planes(const bf16x8* a, const bf16x8* b, f32x16 acc) {
+  if constexpr (PL == 1) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  }
+}
+
+template <int WM, int WN, int TM, int TN, int PL, bool FAST>
+__global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArgs p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = 32 * TM * WM;
+  constexpr int BN = 32 * TN * WN;
+  constexpr int TA = BM * 4 / NT;             // A chunk tasks (8 k each) per thread
+  constexpr int TB = (BN * 4 + NT - 1) / NT;  // B chunk tasks per thread (last may be partial)
+  constexpr bool BFULL = (BN * 4) % NT == 0;
+  static_assert(TA * NT == BM * 4, "A staging must tile the workgroup");
+  constexpr int PA = BM * 4;  // uint4 per A plane
+  constexpr int PB = BN * 4;  // uint4 per B plane
+  constexpr int STAGE = PL * (PA + PB);
+  constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= 2 * STAGE) ? TM : 1;  // epilogue bands per round
+  constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
+  constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  __shared__ uint4 smem[SMEM];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int c = tid & 3;  // this thread's 8-k chunk of every staged row
+
+  // XCD-aware tile order (bijective for any grid size).
+  const int tilesN = (d.Cout + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = wg / tilesN;
+  const int n0 = (wg - mt * tilesN) * BN;
+  const int64_t m0 = (int64_t)mt * BM;
+
+  // Per A task: the im2col row's origin (iy0, ix0) and a pointer to its tap-(0,0) pixel
+  // (+ this thread's chunk); rows past M are parked out of bounds (iy0 = -2^20).
+  int a_iy0[TA], a_ix0[TA];
+  const float* a_ptr[TA];
+  const float* a2_ptr[TA];
+#pragma unroll
+  for (int i = 0; i < TA; ++i) {
+    const int64_t m = m0 + ((tid + NT * i) >> 2);
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int b = (int)(mm / p.HoWo);
+    const int rem = (int)(mm - (int64_t)b * p.HoWo);
+    const int oy = rem / d.Wo;
+    const int ox = rem - oy * d.Wo;
+    a_iy0[i] = ok ? oy * d.stride - d.pad : -(1 << 20);
+    a_ix0[i] = ox * d.stride - d.pad;
+    const int64_t pix = ((int64_t)b * d.H + a_iy0[i]) * d.W + a_ix0[i];
+    a_ptr[i] = d.A + pix * d.lda + c * 8;
+    a2_ptr[i] = d.A2 ? d.A2 + pix * d.lda2 + c * 8 : nullptr;
+  }
+  const uint16_t* b_ptr[TB];
+#pragma unroll
+  for (int i = 0; i < TB; ++i) {
+    const int n = n0 + ((tid + NT * i) >> 2);
+    b_ptr[i] = d.Wt_bf16 + (int64_t)(n < d.Cout ? n : 0) * p.K + c * 8;
+  }
+
+  float4 ra[TA][2];
+  uint4 rb[TB][PL];
+
+  // FAST (Cin % 32 == 0): a 32-deep k-tile lies inside one filter tap, so the tap walk is
+  // wave-uniform scalar state (kh, kw, c0) advanced once per tile.
+  int s_kh = 0, s_kw = 0, s_c0 = 0;
+  auto seek = [&](int kt) {
+    const int k0 = kt * KT;
+    const int tap = k0 / d.Cin;
+    s_c0 = k0 - tap * d.Cin;
+    s_kh = tap / d.KW;
+    s_kw = tap - s_kh * d.KW;
+  };
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * KT;
+    if constexpr (FAST) {
+      const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+      const int64_t off2 = ((int64_t)s_kh * d.W + s_kw) * d.lda2 + s_c0;
+#pragma unroll
+      for (int i = 0; i < TA; ++i) {
+        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+        if ((unsigned)(a_iy0[i] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[i] + s_kw) < (unsigned)d.W) {
+          const float* src = a_ptr[i] + off;
+          v0 = *reinterpret_cast<const float4*>(src);
+          v1 = *reinterpret_cast<const float4*>(src + 4);
+          if (d.A2) {
+            const float* s2 = a2_ptr[i] + off2;
+            const float4 w0 = *reinterpret_cast<const float4*>(s2);
+            const float4 w1 = *reinterpret_cast<const float4*>(s2 + 4);
+            v0.x += w0.x; v0.y += w0.y; v0.z += w0.z; v0.w += w0.w;
+            v1.x += w1.x; v1.y += w1.y; v1.z += w1.z; v1.w += w1.w;
+          }
+        }
+        ra[i][0] = v0;
+        ra[i][1] = v1;
+      }
+#pragma unroll
+      for (int i = 0; i < TB; ++i) {
+        const int t = tid + NT * i;
+        const bool ok = (BFULL || t < BN * 4) && n0 + (t >> 2) < d.Cout;
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          rb[i][pl] = ok ? *reinterpret_cast<const uint4*>(b_ptr[i] + k0 + pl * wps) : make_uint4(0u, 0u, 0u, 0u);
+      }
+      // advance the tap walk to the next k-tile
+      s_c0 += KT;
+      if (s_c0 >= d.Cin) {
+        s_c0 = 0;
+        if (++s_kw == d.KW) {
+          s_kw = 0;
+          ++s_kh;
+        }
+      }
+    } else {  // generic gather (Cin = 3 stem, K = 4 query-pos head): element-wise, k < K checked
+      const int k = k0 + c * 8;
+#pragma unroll
+      for (int i = 0; i < TA; ++i) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int kk = k + j;
+          float v = 0.f;
+          if (kk < p.K) {
+            const int tap = kk / d.Cin;
+            const int ch = kk - tap * d.Cin;
+            const int kh = tap / d.KW;
+            const int kw = tap - kh * d.KW;
+            if ((unsigned)(a_iy0[i] + kh) < (unsigned)d.H && (unsigned)(a_ix0[i] + kw) < (unsigned)d.W) {
+              const int64_t o = ((int64_t)kh * d.W + kw) * d.lda + ch - c * 8;
+              v = a_ptr[i][o];
+              if (d.A2) v += a2_ptr[i][((int64_t)kh * d.W + kw) * d.lda2 + ch - c * 8];
+            }
+          }
+          e[j] = v;
+        }
+        ra[i][0] = make_float4(e[0], e[1], e[2], e[3]);
+        ra[i][1] = make_float4(e[4], e[5], e[6], e[7]);
+      }
+#pragma unroll
+      for (int i = 0; i < TB; ++i) {
+        const int t = tid + NT * i;
+        const bool nok = (BFULL || t < BN * 4) && n0 + (t >> 2) < d.Cout;
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl) {
+          uint16_t e[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e[j] = (nok && k + j < p.K) ? b_ptr[i][k0 + j + pl * wps] : (uint16_t)0;
+          rb[i][pl] = make_uint4(e[0] | (uint32_t)e[1] << 16, e[2] | (uint32_t)e[3] << 16,
+                                 e[4] | (uint32_t)e[5] << 16, e[6] | (uint32_t)e[7] << 16);
+        }
+      }
+    }
+  };
+
+  auto store_tile = [&](uint4* st) {
+#pragma unroll
+    for (int i = 0; i < TA; ++i) {
+      bf16x8 pv[PL];
+      split8<PL>(ra[i][0], ra[i][1], pv);
+      const int row = (tid + NT * i) >> 2;
+#pragma unroll
+      for (int pl = 0; pl < PL; ++pl) *reinterpret_cast<bf16x8*>(st + pl * PA + sw16(row, c)) = pv[pl];
+    }
+#pragma unroll
+    for (int i = 0; i < TB; ++i) {
+      const int t = tid + NT * i;
+      if (BFULL || t < BN * 4) {
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl) st[PL * PA + pl * PB + sw16(t >> 2, c)] = rb[i][pl];
+      }
+    }
+  };
+
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  auto compute_tile = [&](const uint4* st) {
+#pragma unroll
+    for (int s = 0; s < KT / 16; ++s) {
+      bf16x8 fa[TM][PL], fb[TN][PL];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fa[i][pl] = *reinterpret_cast<const bf16x8*>(st + pl * PA + sw16(wm * TM * 32 + i * 32 + r, 2 * s + h));
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + PL * PA + pl * PB +
+                                                       sw16(wn * TN * 32 + j * 32 + r, 2 * s + h));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa[i], fb[j], acc[i][j]);
+    }
+  };
+
+  const int nk_all = (p.K + KT - 1) / KT;
+  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
+  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
+  const int nk = kt1 - kt0;
+  if constexpr (FAST) seek(kt0);
+  if (nk > 0) {
+    load_tile(kt0);
+    store_tile(smem);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) load_tile(kt0 + kt + 1);
+    compute_tile(smem + (kt & 1) * STAGE);
+    if (kt + 1 < nk) store_tile(smem + ((kt + 1) & 1) * STAGE);
+    __syncthreads();
+  }
+
+  float* smemf = reinterpret_cast<float*>(smem);
+  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+                            lane);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant (no A2 addend, Cin % 32 == 0): every operand byte goes global → LDS
+// by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), NS stages deep, one raw
+// s_barrier per k-tile and a counted vmcnt that keeps NS-2 stages in flight across it. A is staged
+// as raw fp32 (the k-tile's 32 channels = 8 × 16-byte chunks per im2col row) and split into bf16
+// planes by each wave at fragment-read time, so the split VALU work interleaves with the MFMAs of
+// the same wave instead of sitting between the load wait and the barrier. The DMA destination is
+// lane-linear (wave base + 16·lane), so the bank swizzle is applied on the SOURCE side: LDS chunk
+// position q of A row r holds global chunk q ^ ((r >> 1) & 7) (conflict-free b128 fragment reads,
+// the fp32 kernel's swizzle), position q of a B row holds chunk q ^ ((r >> 2) & 3) (sw16).
+// Padding taps, rows past M and columns past Cout read a 128-byte zero block instead.
+__device__ float4 g_zero_chunk[8];
+
+template <int PL>
+__device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, bf16x8* out) {
+  split8<PL>(x0, x1, out);
+}
+
+// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left open (gfx9 encoding; n < 64), fenced for the
+// compiler so no LDS access moves across it.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+  asm volatile("" ::: "memory");
+}
+
+// Raw s_barrier (no implied vmcnt(0), unlike __syncthreads), fenced for the compiler.
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One global_load_lds_dwordx4: 16 bytes from each lane's gsrc to LDS byte address
+// lds_base + 16·lane (lds_base wave-uniform). Issued as inline asm so hipcc does not track it:
+// the builtin form makes hipcc wait vmcnt(0) before every later ds_read of the same array, which
+// drains the stage pipeline; completion is counted by hand (wait_vmcnt + raw_barrier).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+template <int WM, int WN, int TM, int TN, int PL, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = 32 * TM * WM;
+  constexpr int BN = 32 * TN * WN;
+  constexpr int CA = BM * 8;  // 16-byte chunks of the fp32 A tile (32 k per row)
+  constexpr int CB = BN * 4;  // 16-byte chunks of one bf16 B plane (32 k per row)
+  constexpr int GA = CA / NT;
+  constexpr int GB = CB / NT;
+  static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
+  constexpr int GLDS = GA + PL * GB;  // DMA instructions per thread per stage
+  constexpr int STAGE = CA + PL * CB;
+  constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
+  constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
+  constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
+  static_assert(NS >= 2 && NS <= 4, "stages");
+  __shared__ uint4 smem[SMEM];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+
+  const int tilesN = (d.Cout + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = wg / tilesN;
+  const int n0 = (wg - mt * tilesN) * BN;
+  const int64_t m0 = (int64_t)mt * BM;
+
+  // A pieces: piece j of this thread covers tile row (j·NT + tid) / 8, LDS position tid % 8,
+  // global chunk (tid % 8) ^ ((row >> 1) & 7) — the same for every j since NT / 8 ≡ 0 (mod 16).
+  const int ca = (tid & 7) ^ (((tid >> 3) >> 1) & 7);
+  int a_iy0[GA], a_ix0[GA];
+  const float* a_ptr[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int64_t m = m0 + ((j * NT + tid) >> 3);
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int b = (int)(mm / p.HoWo);
+    const int rem = (int)(mm - (int64_t)b * p.HoWo);
+    const int oy = rem / d.Wo;
+    const int ox = rem - oy * d.Wo;
+    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
+    a_ix0[j] = ox * d.stride - d.pad;
+    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+  }
+  // B pieces: row (j·NT + tid) / 4, global chunk (tid % 4) ^ ((row >> 2) & 3) (NT / 4 ≡ 0 mod 16).
+  const int cbk = (tid & 3) ^ (((tid >> 2) >> 2) & 3);
+  const uint16_t* b_ptr[GB];
+  bool b_ok[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int n = n0 + ((j * NT + tid) >> 2);
+    b_ok[j] = n < d.Cout;
+    b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
+  }
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+
+  int s_kh = 0, s_kw = 0, s_c0 = 0;
+  const int nk_all = p.K / KT;
+  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
+  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
+  const int nk = kt1 - kt0;
+  {
+    const int k0 = kt0 * KT;
+    const int tap = k0 / d.Cin;
+    s_c0 = k0 - tap * d.Cin;
+    s_kh = tap / d.KW;
+    s_kw = tap - s_kh * d.KW;
+  }
+
+  // Issue the DMA pieces of k-tile kt into stage buffer `buf`, then advance the tap walk.
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int kt, int buf) {
+    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
+      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
+      glds16(src, st + j * NT * 16);
+    }
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl)
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const void* src = b_ok[j] ? static_cast<const void*>(b_ptr[j] + pl * wps + k0)
+                                  : static_cast<const void*>(zero + cbk * 16);
+        glds16(src, st + (CA + pl * CB + j * NT) * 16);
+      }
+    s_c0 += KT;
+    if (s_c0 >= d.Cin) {
+      s_c0 = 0;
+      if (++s_kw == d.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+  };
+
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  auto compute = [&](int buf) {
+    const uint4* st = smem + buf * STAGE;
+#pragma unroll
+    for (int s = 0; s < KT / 16; ++s) {
+      bf16x8 fb[TN][PL];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(wn * TN * 32 + j * 32 + r, 2 * s + h));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 32 + i * 32 + r;
+        const int sz = (row >> 1) & 7;
+        const int c0 = 4 * s + 2 * h;
+        const float4 x0 = *reinterpret_cast<const float4*>(st + row * 8 + (c0 ^ sz));
+        const float4 x1 = *reinterpret_cast<const float4*>(st + row * 8 + ((c0 + 1) ^ sz));
+        bf16x8 fa[PL];
+        split_frag<PL>(x0, x1, fa);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa, fb[j], acc[i][j]);
+      }
+    }
+  };
+
+  // Prologue: stages 0 .. NS-2 in flight.
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(kt0 + t, t);
+  for (int kt = 0; kt < nk; ++kt) {
+    // retire stage kt: stages kt+1 .. min(kt+NS-2, nk-1) may stay in flight
+    const int ahead = (nk - 1 - kt) < (NS - 2) ? (nk - 1 - kt) : (NS - 2);
+    if constexpr (NS >= 4) {
+      if (ahead >= 2) wait_vmcnt<2 * GLDS>();
+      else if (ahead == 1) wait_vmcnt<GLDS>();
+      else wait_vmcnt<0>();
+    } else if constexpr (NS == 3) {
+      if (ahead >= 1) wait_vmcnt<GLDS>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    raw_barrier();
+    if (kt + NS - 1 < nk) issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
+    compute(kt % NS);
+  }
+
+  __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
+  float* smemf = reinterpret_cast<float*>(smem);
+  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+                            lane);
+}
+
+template <int WM, int WN, int TM, int TN, int NS>
+int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
+  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  dim3 grid((unsigned)tiles, 1, a.splits);
+  if (planes == 3)
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
+}
+
+template <int WM, int WN, int TM, int TN>
+int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
+  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  dim3 grid((unsigned)tiles, 1, a.splits);
+  if (planes == 3)
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, a);
+  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3)" : "sp_conv2d(bf16)");
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
+}
+
+}  // namespace
+
+// cfg (register-staged kernel): 1 = 128×128 (2×2 waves of 64×64), 2 = 256×128 (4×2 waves),
+// 3 = 64×128, 4 = 64×64, 5 = 128×256 (2×4 waves), 6 = 128×64;
+// cfg (LDS-DMA kernel, no A2): 11 = 128×128 3 stages, 12 = 256×128 2 stages, 13 = 64×128 3 stages,
+// 14 = 64×64 3 stages, 15 = 128×256 2 stages, 16 = 128×64 3 stages; < 0 = by shape.
+int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  if (!a.fast) {  // generic gather: one small-tile instance per operand mode
+    const int64_t tiles = ((a.M + 63) / 64) * ((a.d.Cout + 63) / 64);
+    dim3 grid((unsigned)tiles, 1, a.splits);
+    if (planes == 3)
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 3, false>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 1, false>), grid, dim3(256), 0, s, a);
+    int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 generic)" : "sp_conv2d(bf16 generic)");
+    if (rc || a.splits == 1) return rc;
+    return launch_splitk_reduce(a, s);
+  }
+  if (cfg >= 11 && cfg <= 16 && !a.d.A2) {
+    switch (cfg) {
+      case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
+      case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
+      case 13: return launch_glds<2, 2, 1, 2, 3>(a, planes, s);
+      case 14: return launch_glds<2, 2, 1, 1, 3>(a, planes, s);
+      case 15: return launch_glds<2, 4, 2, 2, 2>(a, planes, s);
+      default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
+    }
+  }
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || cfg > 16 || (cfg >= 11 && a.d.A2)) {
+    // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
+    // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64.
+    const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };
+    const bool dma = !a.d.A2;
+    if (a.splits > 1) cfg = 4;
+    else if (a.d.Cout <= 64) cfg = dma ? (tiles(128, 64) >= 192 ? 16 : 14) : 4;
+    else if (tiles(256, 128) >= 192) cfg = dma ? 12 : 2;
+    else if (tiles(64, 128) >= 192) cfg = dma ? 13 : 3;
+    else cfg = dma ? 14 : 4;
+    if (cfg >= 11) return launch_mfma16(a, planes, cfg, s);
+  }
+  switch (cfg) {
+    case 1: return launch_cfg<2, 2, 2, 2>(a, planes, s);
+    case 2: return launch_cfg<4, 2, 2, 2>(a, planes, s);
+    case 3: return launch_cfg<2, 2, 1, 2>(a, planes, s);
+    case 5: return launch_cfg<2, 4, 2, 2>(a, planes, s);
+    case 6: return launch_cfg<2, 2, 2, 1>(a, planes, s);
+    default: return launch_cfg<2, 2, 1, 1>(a, planes, s);
+  }
+}
+
+}  // namespace sp

@@ -46,6 +46,27 @@ def bf16_bits(a: np.ndarray) -> np.ndarray:
     return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
 
 
+# precision → (conv GEMM operand mode, linear GEMM operand mode):
+#   "f32"  fp32 MFMA (v_mfma_f32_32x32x2_f32, an exact fmaf chain),
+#   "x3"   fp32 operands as hi/mid/lo bf16 splits on bf16 MFMA (SP_PREC_F32X3; fp32-accurate),
+#   "bf16" bf16 operands, fp32 accumulate (the separately reported bf16 variant).
+PRECISIONS = {
+    "fp32": ("x3", "x3"),
+    "fp32-mfma": ("f32", "f32"),
+    "bf16": ("bf16", "x3"),
+    "bf16-all": ("bf16", "bf16"),
+}
+
+
+def _wkw(wq):
+    """ops.conv2d keyword for a packed GEMM weight form (see Engine._wq)."""
+    if wq is None:
+        return {}
+    if wq.dim() == 2 and wq.shape[0] == 3:
+        return {"wt_planes": wq}
+    return {"wt16": wq}
+
+
 class ConvW:
     __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16")
 
@@ -117,14 +138,12 @@ class Engine:
                  fold_repvgg: bool = True, precision: str = "fp32"):
         from ._lib import lib
 
-        if precision not in ("fp32", "bf16", "bf16-all"):
-            raise ValueError("precision must be 'fp32', 'bf16' (backbone + encoder convs in bf16, the "
-                             "decoder / heads in fp32) or 'bf16-all'")
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
         self.precision = precision
-        self._prec = 0 if precision == "fp32" else 1
-        self._prec_linear = 1 if precision == "bf16-all" else 0
+        self._conv_mode, self._lin_mode = PRECISIONS[precision]
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -143,13 +162,19 @@ class Engine:
         self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
     # ------------------------------------------------------------------ weights
-    def _w16(self, wk: np.ndarray):
-        if self._prec == 0:
+    @staticmethod
+    def _wq(w: torch.Tensor, mode: str):
+        """GEMM operand form of fp32 device weights w [Cout, K]: None (fp32 MFMA), bf16 bit
+        patterns (RNE), or the hi / mid / lo bf16 planes of the fp32-accurate split path."""
+        if mode == "f32":
             return None
-        return torch.from_numpy(bf16_bits(wk).view(np.int16)).to(self.dev)
+        if mode == "bf16":
+            return w.to(torch.bfloat16).view(torch.int16).contiguous()
+        return ops.split_bf16x3(w)
 
     def _mk_conv(self, wk, ci, co, k, sc, sh):
-        return ConvW(_t(wk, self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev), self._w16(wk))
+        w = _t(wk, self.dev)
+        return ConvW(w, ci, co, k, _t(sc, self.dev), _t(sh, self.dev), self._wq(w, self._conv_mode))
 
     def _conv(self, p, conv_key, bn_pre, frozen):
         w = p[conv_key]
@@ -162,8 +187,8 @@ class Engine:
         bs = [p[pre + ".bias"]] + [p[m + ".bias"] for m in more]
         w = np.ascontiguousarray(np.concatenate(ws, 0))
         b = np.concatenate(bs, 0)
-        w16 = self._w16(w) if self._prec_linear else None
-        return LinW(_t(w, self.dev), _t(b, self.dev), w.shape[1], w.shape[0], w16)
+        wd = _t(w, self.dev)
+        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(wd, self._lin_mode))
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -237,9 +262,10 @@ class Engine:
     def _csp(self, p, pre):
         c1 = self._conv(p, pre + ".conv1.conv.weight", pre + ".conv1.norm", False)
         c2 = self._conv(p, pre + ".conv2.conv.weight", pre + ".conv2.norm", False)
-        c12 = ConvW(torch.cat([c1.w, c2.w], 0).contiguous(), c1.cin, c1.cout + c2.cout, 1,
+        w12 = torch.cat([c1.w, c2.w], 0).contiguous()
+        c12 = ConvW(w12, c1.cin, c1.cout + c2.cout, 1,
                     torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous(),
-                    None if c1.w16 is None else torch.cat([c1.w16, c2.w16], 0).contiguous())
+                    self._wq(w12, self._conv_mode))
         reps = []
         for b in range(3):
             q = f"{pre}.bottlenecks.{b}"
@@ -287,11 +313,11 @@ class Engine:
         pad = cw.k // 2
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
-                          workspace=self._buf("splitk", self.SPLITK_ELEMS), wt16=cw.w16, **kw)
+                          workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)
 
     def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None):
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), wt16=lw.w16)
+                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
     def backbone(self, px_nhwc: torch.Tensor, B, H, W):
         """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC)."""

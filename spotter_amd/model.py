@@ -51,9 +51,10 @@ class SpotterForObjectDetection:
     main_input_name = "pixel_values"
 
     def __init__(self, cfg: SpotterConfig, weights: dict | None = None, seed: int = 0,
-                 use_graphs: bool = True):
+                 use_graphs: bool = True, precision: str = "fp32"):
         self.cfg = cfg
         self.use_graphs = use_graphs
+        self.precision = precision  # engine.PRECISIONS key; "fp32" = the fp32-accurate parity path
         self._graphs = {}
         self._seen = set()
         self.config = _Config(cfg)
@@ -112,7 +113,8 @@ class SpotterForObjectDetection:
                     from .engine import Engine
 
                     dev = self._device or torch.device("cuda", torch.cuda.current_device())
-                    self._engine = Engine(self.cfg, self._host_weights(), dev)
+                    self._engine = Engine(self.cfg, self._host_weights(), dev,
+                                          precision=getattr(self, "precision", "fp32"))
         return self._engine
 
     # -- forward ------------------------------------------------------------------

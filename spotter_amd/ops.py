@@ -70,8 +70,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
-           wt16: torch.Tensor | None = None):
-    """wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path."""
+           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None):
+    """wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
+    wt_planes (int16 [3, Cout*K]: the hi / mid / lo bf16 split of the fp32 weights, split_bf16x3)
+    selects the fp32-accurate 3-way-split path (SP_PREC_F32X3)."""
     ho = (h + 2 * pad - k) // stride + 1
     wo = (w + 2 * pad - k) // stride + 1
     m = n * ho * wo
@@ -114,11 +116,20 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     d.ldc = out.ld
     d.out_rows_per_group = rows_per_group
     d.out_group_stride = group_stride
+    if wt16 is not None and wt_planes is not None:
+        raise ValueError("conv: give wt16 (bf16) or wt_planes (f32x3), not both")
     if wt16 is not None:
         if wt16.numel() != cout * k * k * cin or wt16.dtype != torch.int16 or not wt16.is_contiguous():
             raise ValueError("conv bf16 weight shape/dtype mismatch")
         d.precision = 1
         d.Wt_bf16 = wt16.data_ptr()
+    if wt_planes is not None:
+        if (wt_planes.dim() != 2 or wt_planes.shape[0] != 3 or wt_planes.shape[1] != cout * k * k * cin
+                or wt_planes.dtype != torch.int16 or not wt_planes.is_contiguous() or not wt_planes.is_cuda):
+            raise ValueError("conv f32x3 weight planes must be a contiguous int16 CUDA tensor [3, Cout*K]")
+        d.precision = 2
+        d.Wt_bf16 = wt_planes.data_ptr()
+        d.wt_plane_stride = wt_planes.shape[1]
     if workspace is not None:
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
@@ -132,9 +143,20 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
            res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
-           scale=None, workspace=None, wt16=None):
+           scale=None, workspace=None, wt16=None, wt_planes=None):
     return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
-                  res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16)
+                  res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes)
+
+
+def split_bf16x3(w: torch.Tensor) -> torch.Tensor:
+    """fp32 weights → int16 [3, numel] bf16 bit planes hi, mid, lo with w == hi + mid + lo
+    (RNE at each step; both residuals are exact in fp32), the operand format of SP_PREC_F32X3."""
+    w = w.detach().float().reshape(-1)
+    hi = w.to(torch.bfloat16)
+    r1 = w - hi.float()
+    mid = r1.to(torch.bfloat16)
+    lo = (r1 - mid.float()).to(torch.bfloat16)
+    return torch.stack([hi, mid, lo]).view(torch.int16).contiguous()
 
 
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):

@@ -110,8 +110,11 @@ def _bf16(a):
     return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
 
 
+MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16"]
+
+
 @pytest.mark.parametrize("case", CONV_CASES[:7] + [(1, 5, 7, 256, 96, 3, 1, "relu")])
-@pytest.mark.parametrize("cfg", [None, "220", "120", "110"])
+@pytest.mark.parametrize("cfg", MFMA16_CFGS)
 def test_conv2d_bf16_matches_bf16_rounded_reference(dev, case, cfg, monkeypatch):
     """bf16 MFMA path == exact math on bf16-rounded activations and weights (fp32 accumulate)."""
     from spotter_amd import ops
@@ -139,6 +142,78 @@ def test_conv2d_bf16_matches_bf16_rounded_reference(dev, case, cfg, monkeypatch)
                scale=T(sc, dev), shift=T(sh, dev), act=act, res1=view(T(r1.reshape(-1), dev), cout), wt16=w16,
                workspace=ws)
     np.testing.assert_allclose(out.cpu().numpy().reshape(m, cout), ref, rtol=1e-3, atol=1e-3)
+
+
+def _conv64(x, wt, stride, pad):
+    """fp64 conv (NHWC in, [M, Cout] out) — the accuracy yardstick for the fp32 GEMM paths."""
+    xt = torch.from_numpy(x.astype(np.float64)).permute(0, 3, 1, 2)
+    y = torch.nn.functional.conv2d(xt, torch.from_numpy(wt.astype(np.float64)), stride=stride, padding=pad)
+    return y.permute(0, 2, 3, 1).reshape(-1, wt.shape[0]).numpy()
+
+
+F32X3_CASES = CONV_CASES + [(2, 20, 20, 256, 256, 3, 1, None), (4, 16, 16, 1024, 256, 1, 1, None),
+                            (1, 1, 300, 8, 64, 1, 1, None), (1, 1, 777, 256, 1536, 1, 1, None)]
+
+
+@pytest.mark.parametrize("case", F32X3_CASES)
+@pytest.mark.parametrize("cfg", MFMA16_CFGS)
+def test_conv2d_f32x3_is_fp32_accurate(dev, case, cfg, monkeypatch):
+    """SP_PREC_F32X3 (3-way bf16 split, 6 MFMA products) is as accurate as the fp32 MFMA path.
+
+    Both are compared with an fp64 convolution of the same fp32 operands: the split path's max
+    error must stay within 2x the fp32 MFMA path's (an exact fmaf chain) plus 1e-6 relative to
+    the output scale, and under 1e-5 of the output scale outright."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    n, h, w, cin, cout, k, st, _ = case
+    rng = np.random.default_rng(hash(case) % 2**32 + 2)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
+    pad = k // 2
+    ref = _conv64(x, wt, st, pad)
+    m = ref.shape[0]
+    wk = T(wt.transpose(0, 2, 3, 1).reshape(cout, -1), dev)
+    xd = view(T(x.reshape(-1), dev), cin)
+    ws = torch.empty(4 << 20, device=dev)
+    outs = {}
+    for mode in ("fp32", "f32x3"):
+        if mode == "f32x3" and cfg:
+            monkeypatch.setenv("SP_CONV_CFG", cfg)
+        out = torch.empty(m * cout, device=dev)
+        ops.conv2d(xd, n, h, w, cin, wk, cout, k, st, pad, view(out, cout), workspace=ws,
+                   wt_planes=ops.split_bf16x3(wk) if mode == "f32x3" else None)
+        outs[mode] = out.cpu().numpy().reshape(m, cout).astype(np.float64)
+        monkeypatch.delenv("SP_CONV_CFG", raising=False)
+    scale = np.abs(ref).max()
+    e32 = np.abs(outs["fp32"] - ref).max()
+    ex3 = np.abs(outs["f32x3"] - ref).max()
+    assert ex3 <= 2 * e32 + 1e-6 * scale, (ex3, e32, scale)
+    assert ex3 <= 1e-5 * scale, (ex3, scale)
+
+
+def test_conv2d_f32x3_epilogue_and_views(dev):
+    """The split path shares the fused epilogue: BN, residuals, act, A2, row mask, grouped rows."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(8)
+    rows, K, N = 150, 64, 96
+    big = rng.standard_normal((rows, 160)).astype(np.float32)
+    a2 = rng.standard_normal((rows, K)).astype(np.float32)
+    wt = (rng.standard_normal((N, K)) / 8).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    mask = (rng.uniform(size=50) > 0.3).astype(np.float32)
+    x = big[:, 32:32 + K] + a2
+    ref = ((x @ wt.T) * mask[np.arange(rows) % 50][:, None] + b).astype(np.float32)
+    out = torch.zeros(3 * 70 * N, device=dev)
+    wd = T(wt, dev)
+    ops.conv2d(V(T(big.reshape(-1), dev), 32, 160), 1, 1, rows, K, wd, N, 1, 1, 0,
+               V(out, 11 * N, N), shift=T(b, dev), a2=V(T(a2.reshape(-1), dev), 0, K),
+               row_scale=T(mask, dev), rows_per_group=50, group_stride=70 * N, wt_planes=ops.split_bf16x3(wd))
+    got = out.cpu().numpy().reshape(3, 70, N)[:, 11:61].reshape(rows, N)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4)
+    assert np.all(out.cpu().numpy().reshape(3, 70, N)[:, :11] == 0)
 
 
 def test_conv2d_strided_views_rowscale_a2_grouped(dev):

@@ -43,13 +43,14 @@ def match_detections(got, exp_scores, exp_labels, exp_boxes):
         used.add(cand[0])
 
 
-def run_case(preset, tag=None):
+def run_case(preset, tag=None, precision="fp32"):
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
     from spotter_amd.config import PRESETS
 
     g = np.load(os.path.join(GOLD, f"{tag or preset + '_640'}.npz"))
     size = int(g["size"])
-    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)  # eager: read topk from _ws
+    # eager: read topk from _ws
+    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False, precision=precision)
     proc = SpotterImageProcessor(size={"height": size, "width": size})
     imgs = load_images(g)
     off = 0
@@ -81,12 +82,15 @@ def run_case(preset, tag=None):
     return model
 
 
-def test_r18vd_matches_hf_goldens():
-    run_case("r18vd")
+# "fp32": GEMMs as 3-way bf16 splits (SP_PREC_F32X3, the default path); "fp32-mfma": v_mfma_f32_32x32x2_f32.
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
+def test_r18vd_matches_hf_goldens(precision):
+    run_case("r18vd", precision=precision)
 
 
-def test_r101vd_matches_hf_goldens():
-    run_case("r101vd")
+@pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
+def test_r101vd_matches_hf_goldens(precision):
+    run_case("r101vd", precision=precision)
 
 
 def test_r101vd_1280_mixed_resolution_matches_hf_goldens():

@@ -1,7 +1,15 @@
-"""Micro-bench of sp_conv2d on the R101vd@640 bs32 shapes that dominate the step (per-shape TFLOP/s)."""
+"""Micro-bench of sp_conv2d on the R101vd@640 bs32 shapes that dominate the step (per-shape TFLOP/s).
+
+    python tools/conv_bench.py [--prec fp32,f32x3,bf16] [--cfgs -,1,2] [--shapes 0,1,2] [--reps 20]
+
+cfg "-" = the library's own tile choice; other values go to SP_CONV_CFG (fp32 kernel: "<TM><TN><DB>",
+bf16 / f32x3 kernels: 1..6). Prints one JSON line per (shape, precision, cfg), plus the step-weighted
+total for the default choice.
+"""
+import argparse
 import json
-import sys
 import os
+import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -9,50 +17,58 @@ import torch
 from spotter_amd import ops
 from spotter_amd.ops import view
 
-# (n, h, w, cin, cout, k, stride, act, residual)
+# (n, h, w, cin, cout, k, stride, act, residual, launches per bs32 step)  — from bench.py --detail
 SHAPES = [
-    (32, 40, 40, 256, 256, 3, 1, "relu", False),     # stage3 3x3        14.7 ms/step
-    (32, 80, 80, 384, 384, 3, 1, None, False),       # CCFM 3x3 @80²      13.4
-    (32, 40, 40, 256, 1024, 1, 1, "relu", True),     # stage3 expand      12.0
-    (32, 40, 40, 1024, 256, 1, 1, "relu", False),    # stage3 reduce       7.5
-    (32, 160, 160, 64, 256, 1, 1, "relu", True),     # stage0 expand       5.0
-    (32, 80, 80, 128, 512, 1, 1, "relu", True),      # stage1 expand       3.2
-    (32, 80, 80, 384, 384, 1, 1, "silu", True),      # CCFM 1x1 @80²       3.0
-    (1, 1, 268800, 256, 1536, 1, 1, None, False),    # value_all           2.7
-    (32, 20, 20, 512, 2048, 1, 1, "relu", True),     # stage4 expand
-    (1, 1, 9600, 256, 256, 1, 1, None, True),        # decoder linear
-    (64, 40, 40, 256, 256, 3, 1, "relu", False),     # 10: stage3 3x3 at 2x batch (tail test)
-    (128, 40, 40, 256, 256, 3, 1, "relu", False),    # 11: 4x batch
-    (32, 320, 320, 32, 32, 3, 1, "relu", False),     # 12: stem conv2 (N=32)
-    (32, 640, 640, 3, 32, 3, 2, "relu", False),      # 13: stem conv1 (Cin=3)
+    (32, 80, 80, 384, 384, 3, 1, None, False, 3),       # 0  CCFM 3x3 @80²         13.3 ms/step fp32
+    (32, 40, 40, 256, 256, 3, 1, "relu", False, 22),    # 1  stage3 3x3            12.4
+    (32, 40, 40, 384, 384, 3, 1, None, False, 6),       # 2  CCFM 3x3 @40²          7.2
+    (32, 40, 40, 256, 1024, 1, 1, "relu", True, 23),    # 3  stage3 expand          6.8
+    (32, 40, 40, 1024, 256, 1, 1, "relu", False, 22),   # 4  stage3 reduce          5.8
+    (32, 80, 80, 768, 768, 1, 1, None, False, 1),       # 5  CCFM 1x1 768 @80²      2.1
+    (1, 1, 268800, 256, 1536, 1, 1, None, False, 1),    # 6  decoder value_all      2.0
+    (32, 160, 160, 256, 64, 1, 1, "relu", False, 4),    # 7  stage0 reduce (K=64→N)  1.8 (K=256)
+    (32, 160, 160, 64, 64, 3, 1, "relu", False, 3),     # 8  stage0 3x3             1.8
+    (32, 80, 80, 128, 128, 3, 1, "relu", False, 3),     # 9  stage1 3x3             1.7
+    (32, 80, 80, 128, 512, 1, 1, "relu", True, 4),      # 10 stage1 expand          1.4
+    (32, 20, 20, 512, 512, 3, 1, "relu", False, 2),     # 11 stage4 3x3             1.2
+    (32, 320, 320, 32, 64, 3, 1, "relu", False, 1),     # 12 stem conv3             1.2
+    (32, 320, 320, 32, 32, 3, 1, "relu", False, 1),     # 13 stem conv2             1.1
+    (1, 1, 9600, 256, 256, 1, 1, None, True, 32),       # 14 decoder linear          0.8
+    (32, 640, 640, 3, 32, 3, 2, "relu", False, 1),      # 15 stem conv1 (Cin=3)
+    (32, 160, 160, 64, 256, 1, 1, "relu", True, 4),     # 16 stage0 expand
 ]
 
 
-def bench_one(dev, shape, cfg):
-    n, h, w, cin, cout, k, st, act, resid = shape
-    if cfg:
+def bench_one(dev, shape, prec, cfg, reps):
+    n, h, w, cin, cout, k, st, act, resid, _ = shape
+    if cfg and cfg != "-":
         os.environ["SP_CONV_CFG"] = cfg
     else:
         os.environ.pop("SP_CONV_CFG", None)
     pad = k // 2
     ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
     m = n * ho * wo
-    x = torch.randn(n * h * w * cin, device=dev)
-    wt = torch.randn(cout * k * k * cin, device=dev) * (1.0 / (cin * k * k) ** 0.5)
-    sc = torch.rand(cout, device=dev) + 0.5
-    sh = torch.randn(cout, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(n * h * w * cin, device=dev, generator=g)
+    wt = torch.randn(cout * k * k * cin, device=dev, generator=g) * (1.0 / (cin * k * k) ** 0.5)
+    sc = torch.rand(cout, device=dev, generator=g) + 0.5
+    sh = torch.randn(cout, device=dev, generator=g)
     out = torch.empty(m * cout, device=dev)
-    r1 = torch.randn(m * cout, device=dev) if resid else None
+    r1 = torch.randn(m * cout, device=dev, generator=g) if resid else None
+    kw = {}
+    if prec == "bf16":
+        kw["wt16"] = wt.to(torch.bfloat16).view(torch.int16).contiguous()
+    elif prec == "f32x3":
+        kw["wt_planes"] = ops.split_bf16x3(wt)
 
     def run():
         ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, st, pad, view(out, cout), scale=sc, shift=sh,
-                   act=act, res1=view(r1, cout) if resid else None)
+                   act=act, res1=view(r1, cout) if resid else None, **kw)
 
     for _ in range(3):
         run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
     e0.record()
     for _ in range(reps):
         run()
@@ -60,17 +76,28 @@ def bench_one(dev, shape, cfg):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
     fl = 2.0 * m * cout * cin * k * k
-    return {"shape": [n, h, w, cin, cout, k, st], "cfg": cfg, "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1)}
+    return {"shape": list(shape[:7]), "prec": prec, "cfg": cfg, "ms": round(ms, 4),
+            "tflops": round(fl / ms / 1e9, 1), "ms_per_step": round(ms * shape[9], 3)}
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--prec", default="fp32")
+    ap.add_argument("--cfgs", default="-")
+    ap.add_argument("--shapes", default=None)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    cfgs = sys.argv[1].split(",") if len(sys.argv) > 1 and sys.argv[1] != "-" else [None]
-    which = [int(i) for i in sys.argv[2].split(",")] if len(sys.argv) > 2 else range(len(SHAPES))
+    which = [int(i) for i in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
+    tot = {}
     for si in which:
-        shape = SHAPES[si]
-        for cfg in cfgs:
-            print(json.dumps(bench_one(dev, shape, cfg)), flush=True)
+        for prec in a.prec.split(","):
+            for cfg in a.cfgs.split(","):
+                r = bench_one(dev, SHAPES[si], prec, cfg, a.reps)
+                print(json.dumps(r), flush=True)
+                if cfg == "-":
+                    tot[prec] = tot.get(prec, 0.0) + r["ms_per_step"]
+    print(json.dumps({"step_weighted_ms_default_cfg": {k: round(v, 2) for k, v in tot.items()}}), flush=True)
 
 
 if __name__ == "__main__":
