@@ -277,8 +277,14 @@ def main():
         ach = c["flops"] / (c["busy"] * 1e-3) / 1e12
         alg_bytes = c["bytes"] / c["n"]
         traffic, tnote = load_traffic(args, alg_bytes)
-        kname = ("conv_gemm_bf16_kernel (v_mfma_f32_32x32x16_bf16 implicit GEMM; fp32 decoder GEMMs included)" if bf
-                 else "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)")
+        if args.precision == "fp32-mfma":
+            kname = "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)"
+        elif bf:
+            kname = ("conv_glds_kernel<PL=1> (bf16 operands, v_mfma_f32_32x32x16_bf16 implicit GEMM, LDS-DMA staged; "
+                     + ("decoder linears f32x3)" if args.precision == "bf16" else "decoder linears bf16)"))
+        else:
+            kname = ("conv_glds_kernel<PL=3> (fp32 operands split hi/mid/lo bf16, 6 v_mfma_f32_32x32x16_bf16 "
+                     "per 32x32x16 block, implicit GEMM, LDS-DMA staged)")
         roof = {"bound": "mfma", "kernel": kname,
                 "achieved": round(ach, 2), "peak": conv_peak, "unit": "TFLOP/s",
                 "frac": round(ach / conv_peak, 4), "traffic": traffic,
@@ -292,6 +298,11 @@ def main():
                         "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
         if tnote:
             roof["traffic_source"] = tnote
+        if args.precision == "fp32":
+            # the fp32-accurate split runs 6 bf16 MFMAs per fp32 product block: the matrix pipe's own rate
+            roof["mfma_issue"] = {"instr": "v_mfma_f32_32x32x16_bf16", "mfma_per_fp32_block": 6,
+                                  "achieved": round(6 * ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)}
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:

@@ -549,6 +549,244 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   return launch_splitk_reduce(a, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Software-pipelined LDS-DMA variant: as conv_glds_kernel, plus the fragment loads (ds_read +
+// bf16 split) of k16 step t+1 are issued between the MFMAs of step t (sched_group_barrier
+// interleave), so one wave per SIMD keeps its matrix pipe fed: the split VALU work and the LDS
+// read latency hide under the MFMA chain. One raw barrier per k-tile sits between its two k16
+// steps: by then every wave has consumed its reads of the buffer being refilled, and stage kt+1
+// has been waited for (vmcnt counted; NS-3 stages stay in flight) so the second half can prefetch
+// the next tile's first step.
+template <int WM, int WN, int TM, int TN, int PL, int NS>
+__global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = 32 * TM * WM;
+  constexpr int BN = 32 * TN * WN;
+  constexpr int CA = BM * 8;
+  constexpr int CB = BN * 4;
+  constexpr int GA = CA / NT;
+  constexpr int GB = CB / NT;
+  static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
+  constexpr int GLDS = GA + PL * GB;
+  constexpr int STAGE = CA + PL * CB;
+  constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
+  constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
+  constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
+  static_assert(NS >= 3 && NS <= 4, "stages");
+  __shared__ uint4 smem[SMEM];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+
+  const int tilesN = (d.Cout + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = wg / tilesN;
+  const int n0 = (wg - mt * tilesN) * BN;
+  const int64_t m0 = (int64_t)mt * BM;
+
+  const int ca = (tid & 7) ^ (((tid >> 3) >> 1) & 7);
+  int a_iy0[GA], a_ix0[GA];
+  const float* a_ptr[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int64_t m = m0 + ((j * NT + tid) >> 3);
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int b = (int)(mm / p.HoWo);
+    const int rem = (int)(mm - (int64_t)b * p.HoWo);
+    const int oy = rem / d.Wo;
+    const int ox = rem - oy * d.Wo;
+    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
+    a_ix0[j] = ox * d.stride - d.pad;
+    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+  }
+  const int cbk = (tid & 3) ^ (((tid >> 2) >> 2) & 3);
+  const uint16_t* b_ptr[GB];
+  bool b_ok[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int n = n0 + ((j * NT + tid) >> 2);
+    b_ok[j] = n < d.Cout;
+    b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
+  }
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+
+  int s_kh = 0, s_kw = 0, s_c0 = 0;
+  const int nk_all = p.K / KT;
+  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
+  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
+  const int nk = kt1 - kt0;
+  {
+    const int k0 = kt0 * KT;
+    const int tap = k0 / d.Cin;
+    s_c0 = k0 - tap * d.Cin;
+    s_kh = tap / d.KW;
+    s_kw = tap - s_kh * d.KW;
+  }
+
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int kt, int buf) {
+    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
+      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
+      glds16(src, st + j * NT * 16);
+    }
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl)
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const void* src = b_ok[j] ? static_cast<const void*>(b_ptr[j] + pl * wps + k0)
+                                  : static_cast<const void*>(zero + cbk * 16);
+        glds16(src, st + (CA + pl * CB + j * NT) * 16);
+      }
+    s_c0 += KT;
+    if (s_c0 >= d.Cin) {
+      s_c0 = 0;
+      if (++s_kw == d.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+  };
+
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  int a_row[TM], a_sz[TM], b_row[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    a_row[i] = (wm * TM * 32 + i * 32 + r) * 8;
+    a_sz[i] = ((wm * TM * 32 + i * 32 + r) >> 1) & 7;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) b_row[j] = wn * TN * 32 + j * 32 + r;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  bf16x8 fa0[TM][PL], fb0[TN][PL], fa1[TM][PL], fb1[TN][PL];
+
+  // fragments of k16 step s (0/1) of stage buffer `buf`
+  auto frags = [&](int buf, int s, bf16x8 (&fa)[TM][PL], bf16x8 (&fb)[TN][PL]) {
+    const uint4* st = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int pl = 0; pl < PL; ++pl)
+        fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(b_row[j], 2 * s + h));
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int c0 = 4 * s + 2 * h;
+      const float4 x0 = *reinterpret_cast<const float4*>(st + a_row[i] + (c0 ^ a_sz[i]));
+      const float4 x1 = *reinterpret_cast<const float4*>(st + a_row[i] + ((c0 + 1) ^ a_sz[i]));
+      split8<PL>(x0, x1, fa[i]);
+    }
+  };
+  auto mma = [&](const bf16x8 (&fa)[TM][PL], const bf16x8 (&fb)[TN][PL]) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa[i], fb[j], acc[i][j]);
+  };
+  // per MFMA of the current step: first the next step's ds_reads (2 per gap), then its VALU
+  constexpr int NMF = TM * TN * (PL == 3 ? 6 : 1);
+  constexpr int NDS = TM * 2 + TN * PL;
+  constexpr int NVALU = TM * (PL == 3 ? 48 : 8) + 8;
+  constexpr int VSTART = NMF > 4 ? 2 : 1;
+  constexpr int VPER = (NVALU + (NMF - VSTART) - 1) / (NMF - VSTART > 0 ? NMF - VSTART : 1);
+  auto interleave = [&]() {
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i < (NDS + 1) / 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      if (i >= VSTART) __builtin_amdgcn_sched_group_barrier(0x002, VPER, 0);
+    }
+  };
+
+  // prologue: stages 0 .. NS-2 in flight; stage 0 landed for everyone; step-0 fragments
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(kt0 + t, t);
+  if (nk > 0) {
+    if (nk >= NS - 1) {
+      wait_vmcnt<(NS - 2) * GLDS>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    raw_barrier();
+    frags(0, 0, fa0, fb0);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt % NS;
+    const int nxt = (kt + 1) % NS;
+    // half A: MFMAs of step (kt, 0) ‖ fragments of step (kt, 1)
+    frags(cur, 1, fa1, fb1);
+    mma(fa0, fb0);
+    interleave();
+    // stage kt+1 landed (stages up to kt+NS-2 issued; NS-3 of them may stay in flight)
+    if constexpr (NS == 4) {
+      if (kt + 2 < nk) wait_vmcnt<GLDS>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    raw_barrier();  // every wave is past its reads of buffer (kt-1) % NS → refill it
+    if (kt + NS - 1 < nk) issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
+    // half B: MFMAs of step (kt, 1) ‖ fragments of step (kt+1, 0) (a harmless stale read after the last tile)
+    frags(nxt, 0, fa0, fb0);
+    mma(fa1, fb1);
+    interleave();
+  }
+
+  __syncthreads();
+  float* smemf = reinterpret_cast<float*>(smem);
+  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+                            lane);
+}
+
+template <int WM, int WN, int TM, int TN, int NS>
+int launch_pipe(const ConvArgs& a, int planes, hipStream_t s) {
+  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
+  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  dim3 grid((unsigned)tiles, 1, a.splits);
+  // NS stages of the fp32 A tile + PL bf16 B planes must fit the 160 KiB LDS
+  constexpr bool fits3 = NS * (BM * 8 + 3 * BN * 4) * 16 <= 163840;
+  if (planes == 3) {
+    if constexpr (fits3) {
+      hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+    } else {
+      set_error("sp_conv2d: pipe tile %dx%d with %d stages does not fit LDS in f32x3 mode", BM, BN, NS);
+      return -1;
+    }
+  } else {
+    hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+  }
+  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 pipe)" : "sp_conv2d(bf16 pipe)");
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
+}
+
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
@@ -585,6 +823,16 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
+  if (cfg >= 21 && cfg <= 26 && !a.d.A2) {
+    switch (cfg) {
+      case 21: return launch_pipe<2, 2, 2, 2, 4>(a, planes, s);   // 128×128, 4 stages
+      case 22: return launch_pipe<2, 2, 2, 4, 3>(a, planes, s);   // 128×256 (wave 64×128)
+      case 23: return launch_pipe<4, 1, 2, 4, 3>(a, planes, s);   // 256×128 (wave 64×128)
+      case 24: return launch_pipe<2, 2, 2, 2, 3>(a, planes, s);   // 128×128, 3 stages
+      case 25: return launch_pipe<4, 2, 2, 2, 3>(a, planes, s);   // 256×128, 8 waves
+      default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
+    }
+  }
   if (cfg >= 11 && cfg <= 16 && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
@@ -595,7 +843,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || cfg > 16 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 16 && cfg < 21) || cfg > 26 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64.
     const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };

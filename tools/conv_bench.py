@@ -93,7 +93,11 @@ def main():
     for si in which:
         for prec in a.prec.split(","):
             for cfg in a.cfgs.split(","):
-                r = bench_one(dev, SHAPES[si], prec, cfg, a.reps)
+                try:
+                    r = bench_one(dev, SHAPES[si], prec, cfg, a.reps)
+                except RuntimeError as e:  # a tile config the shape/mode cannot use (e.g. LDS overflow)
+                    print(json.dumps({"shape": SHAPES[si][:7], "prec": prec, "cfg": cfg, "skipped": str(e)}), flush=True)
+                    continue
                 print(json.dumps(r), flush=True)
                 if cfg == "-":
                     tot[prec] = tot.get(prec, 0.0) + r["ms_per_step"]

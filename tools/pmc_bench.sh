@@ -12,4 +12,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv 
   -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/write" -o pmc \
   -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1
-python3 tools/pmc_reduce.py "$OUT" $ARGS
+python3 tools/pmc_reduce.py "$OUT" $ARGS > "$OUT/traffic.json"; cat "$OUT/traffic.json"
