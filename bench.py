@@ -112,6 +112,18 @@ class KernelEventRecorder:
                  "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1)} for k, v in agg.items()]
         return sorted(rows, key=lambda r: -r["ms"])
 
+    def conv_modes(self):
+        """GEMM operand mode (shape[5]: f32 / bf16 / x3) -> dict(flops, ms = summed launch durations, n)."""
+        out = {}
+        for k, e0, e1, f, nb, shp in self.recs:
+            if k != "conv" or not shp or len(shp) < 6:
+                continue
+            c = out.setdefault(shp[5], {"flops": 0, "ms": 0.0, "n": 0})
+            c["flops"] += f
+            c["ms"] += e0.elapsed_time(e1)
+            c["n"] += 1
+        return out
+
     def classes(self):
         """kind -> dict(ms = sum of launch durations, busy = union of launch intervals, flops, bytes, n)."""
         out = {}
@@ -284,7 +296,8 @@ def main():
                      + ("decoder linears f32x3)" if args.precision == "bf16" else "decoder linears bf16)"))
         else:
             kname = ("conv_glds_kernel<PL=3> (fp32 operands split hi/mid/lo bf16, 6 v_mfma_f32_32x32x16_bf16 "
-                     "per 32x32x16 block, implicit GEMM, LDS-DMA staged)")
+                     "per 32x32x16 block, implicit GEMM, LDS-DMA staged) + conv_gemm_kernel (fp32 "
+                     "v_mfma_f32_32x32x2f32) on thin layers and decoder linears; split in 'modes'")
         roof = {"bound": "mfma", "kernel": kname,
                 "achieved": round(ach, 2), "peak": conv_peak, "unit": "TFLOP/s",
                 "frac": round(ach / conv_peak, 4), "traffic": traffic,
@@ -298,11 +311,21 @@ def main():
                         "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
         if tnote:
             roof["traffic_source"] = tnote
-        if args.precision == "fp32":
-            # the fp32-accurate split runs 6 bf16 MFMAs per fp32 product block: the matrix pipe's own rate
-            roof["mfma_issue"] = {"instr": "v_mfma_f32_32x32x16_bf16", "mfma_per_fp32_block": 6,
-                                  "achieved": round(6 * ach, 1), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)}
+        # per operand mode: share of the class's FLOPs and time, and the matrix pipe's own instruction rate
+        # (the fp32-accurate split issues 6 bf16 MFMAs per fp32 32x32x16 product block)
+        modes = {}
+        per_mfma = {"x3": (6, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
+                    "bf16": (1, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
+                    "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS)}
+        for md, c in rec.conv_modes().items():
+            a = c["flops"] / (c["ms"] * 1e-3) / 1e12
+            mult, instr, pk = per_mfma[md]
+            modes[md] = {"flop_share": round(c["flops"] / max(1, cl["conv"]["flops"]), 4),
+                         "ms_per_step": round(c["ms"] / args.steps, 3), "launches_per_step": c["n"] // args.steps,
+                         "achieved": round(a, 2), "unit": "TFLOP/s",
+                         "mfma_issue": {"instr": instr, "mfma_per_fp32_block": mult,
+                                        "achieved": round(mult * a, 1), "peak": pk, "frac": round(mult * a / pk, 4)}}
+        roof["modes"] = modes
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:

@@ -833,17 +833,21 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (cfg >= 11 && cfg <= 16 && !a.d.A2) {
+  if (cfg >= 11 && cfg <= 20 && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
       case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
       case 13: return launch_glds<2, 2, 1, 2, 3>(a, planes, s);
       case 14: return launch_glds<2, 2, 1, 1, 3>(a, planes, s);
       case 15: return launch_glds<2, 4, 2, 2, 2>(a, planes, s);
+      case 17: return launch_glds<4, 1, 2, 4, 2>(a, planes, s);  // 256×128, 4 waves of 64×128
+      case 18: return launch_glds<2, 2, 2, 4, 2>(a, planes, s);  // 128×256, 4 waves of 64×128
+      case 19: return launch_glds<2, 1, 2, 4, 2>(a, planes, s);  // 128×128, 2 waves of 64×128, 2 stages
+      case 20: return launch_glds<2, 1, 2, 4, 3>(a, planes, s);  // 128×128, 2 waves of 64×128
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 16 && cfg < 21) || cfg > 26 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || cfg > 26 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64.
     const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };

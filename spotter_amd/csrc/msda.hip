@@ -63,6 +63,84 @@ __global__ __launch_bounds__(256) void msda_kernel(const sp_msda_desc d) {
   d.out[row * d.ld_out + h * d.head_dim + c] = out;
 }
 
+// Vectorised form (the decoder's layout: C = heads·Dh with Dh % 4 == 0, 16-byte aligned rows):
+// one lane per 4 channels of one head, C/4 lanes per query (64 = one wave per query at C = 256),
+// so every bilinear corner is one 16-byte load per lane and a wave-instruction covers the corner
+// rows of all 8 heads. Out-of-range corners read a clamped in-range pixel with weight 0 instead of
+// branching, so the 4·L·P loads of a lane are independent and stay in flight together. The grid is
+// remapped XCD-major: each XCD walks a contiguous run of queries (a few whole images), which keeps
+// an image's value rows in that XCD's L2 while its queries are being sampled.
+__global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, int lanes_per_q) {
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int qpw = 256 / lanes_per_q;
+  const int64_t row = (int64_t)wg * qpw + threadIdx.x / lanes_per_q;  // b*Q + q
+  if (row >= (int64_t)d.B * d.Q) return;
+  const int t = threadIdx.x % lanes_per_q;
+  const int lph = d.head_dim >> 2;  // lanes per head
+  const int h = t / lph;
+  const int c = (t - h * lph) * 4;
+  const int b = (int)(row / d.Q);
+  const int LP = d.levels * d.points;
+  const float* offs = d.off_aw + row * d.ld_off_aw + (int64_t)h * LP * 2;
+  const float* logit = d.off_aw + row * d.ld_off_aw + (int64_t)d.heads * LP * 2 + (int64_t)h * LP;
+  const float rx = d.ref[row * 4 + 0], ry = d.ref[row * 4 + 1];
+  const float rw = d.ref[row * 4 + 2], rh = d.ref[row * 4 + 3];
+  float mx = -INFINITY;
+  for (int i = 0; i < LP; ++i) mx = fmaxf(mx, logit[i]);
+  float den = 0.f;
+  for (int i = 0; i < LP; ++i) den += expf(logit[i] - mx);
+  const float nps = 1.0f / (float)d.points;
+  const float* vbase = d.value + (int64_t)b * d.S * d.ld_value + d.value_col + h * d.head_dim + c;
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int l = 0; l < d.levels; ++l) {
+    const int H = d.level_h[l], W = d.level_w[l];
+    const float* vl = vbase + (int64_t)d.level_start[l] * d.ld_value;
+#pragma unroll 4
+    for (int p = 0; p < d.points; ++p) {
+      const int i = l * d.points + p;
+      const float a = expf(logit[i] - mx) / den;
+      const float lx = rx + offs[2 * i] * nps * rw * d.offset_scale;
+      const float ly = ry + offs[2 * i + 1] * nps * rh * d.offset_scale;
+      const float gx = 2.0f * lx - 1.0f;
+      const float gy = 2.0f * ly - 1.0f;
+      const float ix = ((gx + 1.0f) * W - 1.0f) / 2.0f;
+      const float iy = ((gy + 1.0f) * H - 1.0f) / 2.0f;
+      const float x0 = floorf(ix), y0 = floorf(iy);
+      const float x1 = x0 + 1.0f, y1 = y0 + 1.0f;
+      float wnw = (x1 - ix) * (y1 - iy);
+      float wne = (ix - x0) * (y1 - iy);
+      float wsw = (x1 - ix) * (iy - y0);
+      float wse = (ix - x0) * (iy - y0);
+      // far-out locations: keep the integer math in range (every corner is invalid there anyway)
+      const int xi0 = (int)fminf(fmaxf(x0, -2.0f), (float)W);
+      const int yi0 = (int)fminf(fmaxf(y0, -2.0f), (float)H);
+      const bool vx0 = xi0 >= 0 && xi0 < W, vx1 = xi0 + 1 >= 0 && xi0 + 1 < W;
+      const bool vy0 = yi0 >= 0 && yi0 < H, vy1 = yi0 + 1 >= 0 && yi0 + 1 < H;
+      const int cx0 = min(max(xi0, 0), W - 1), cx1 = min(max(xi0 + 1, 0), W - 1);
+      const int cy0 = min(max(yi0, 0), H - 1), cy1 = min(max(yi0 + 1, 0), H - 1);
+      const float4 vnw = *reinterpret_cast<const float4*>(vl + ((int64_t)cy0 * W + cx0) * d.ld_value);
+      const float4 vne = *reinterpret_cast<const float4*>(vl + ((int64_t)cy0 * W + cx1) * d.ld_value);
+      const float4 vsw = *reinterpret_cast<const float4*>(vl + ((int64_t)cy1 * W + cx0) * d.ld_value);
+      const float4 vse = *reinterpret_cast<const float4*>(vl + ((int64_t)cy1 * W + cx1) * d.ld_value);
+      // an invalid corner adds exactly +0 (same sum as skipping it, M2:79-81 zeros padding)
+      wnw = (vy0 && vx0) ? wnw : 0.f;
+      wne = (vy0 && vx1) ? wne : 0.f;
+      wsw = (vy1 && vx0) ? wsw : 0.f;
+      wse = (vy1 && vx1) ? wse : 0.f;
+      float4 s;
+      s.x = vnw.x * wnw; s.y = vnw.y * wnw; s.z = vnw.z * wnw; s.w = vnw.w * wnw;
+      s.x += vne.x * wne; s.y += vne.y * wne; s.z += vne.z * wne; s.w += vne.w * wne;
+      s.x += vsw.x * wsw; s.y += vsw.y * wsw; s.z += vsw.z * wsw; s.w += vsw.w * wsw;
+      s.x += vse.x * wse; s.y += vse.y * wse; s.z += vse.z * wse; s.w += vse.w * wse;
+      out.x += s.x * a; out.y += s.y * a; out.z += s.z * a; out.w += s.w * a;
+    }
+  }
+  *reinterpret_cast<float4*>(d.out + row * d.ld_out + h * d.head_dim + c) = out;
+}
+
 }  // namespace
 }  // namespace sp
 
@@ -78,7 +156,16 @@ extern "C" int sp_msda(const sp_msda_desc* d, void* stream) {
     total += d->level_h[l] * d->level_w[l];
   }
   SP_ARG_CHECK(total == d->S, "sp_msda: Σ H·W = %d != S = %d", total, d->S);
-  hipLaunchKernelGGL(msda_kernel, dim3((unsigned)((int64_t)d->B * d->Q)), dim3(d->heads * d->head_dim),
-                     0, as_stream(stream), *d);
+  const int C = d->heads * d->head_dim;
+  const bool vec = d->head_dim % 4 == 0 && 256 % (C / 4) == 0 && d->ld_value % 4 == 0 && d->value_col % 4 == 0 &&
+                   d->ld_out % 4 == 0 && ((uintptr_t)d->value & 15) == 0 && ((uintptr_t)d->out & 15) == 0;
+  const int64_t rows = (int64_t)d->B * d->Q;
+  if (vec) {
+    const int lanes = C / 4, qpw = 256 / lanes;
+    hipLaunchKernelGGL(msda_vec_kernel, dim3((unsigned)((rows + qpw - 1) / qpw)), dim3(256), 0, as_stream(stream),
+                       *d, lanes);
+  } else {
+    hipLaunchKernelGGL(msda_kernel, dim3((unsigned)rows), dim3(C), 0, as_stream(stream), *d);
+  }
   return check_launch("sp_msda");
 }

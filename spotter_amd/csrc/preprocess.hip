@@ -11,6 +11,7 @@
 // then the vertical pass + rescale + NCHW store (coalesced along x). The
 // coefficient tables are computed on the host with Pillow's double-precision
 // recipe and cached on the device per (in, out) size.
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -23,7 +24,7 @@ namespace {
 
 constexpr int kPrecisionBits = 32 - 8 - 2;
 constexpr int kLdsBytes = 48 * 1024;
-constexpr int kMaxImgs = 16;
+constexpr int kMaxImgs = 32;
 
 struct Coeffs {
   int ksize = 0;
@@ -116,50 +117,65 @@ __device__ __forceinline__ int clip8(int acc) {
   return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
+// Thread mapping: every pass walks output columns with the threads and rows with a loop, so the
+// per-column coefficients are loaded once and reused down the band (no index divisions).
 __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
   __shared__ uint8_t tmp[kLdsBytes];
+  __shared__ float lut[256];
   const PreImg& im = a.img[blockIdx.y];
   const int tile = blockIdx.x;
   if (tile >= im.ntiles) return;
+  // rescale table: f32(f64(v) * (1/255)), exactly IT:118-122's arithmetic
+  lut[threadIdx.x] = (float)((double)threadIdx.x * (1.0 / 255.0));
   const int ow = a.out_w, oh = a.out_h;
   const int y0 = tile * im.rows_per_tile;
   const int y1 = min(y0 + im.rows_per_tile, oh);
   const int r0 = im.vb[2 * y0];
   const int r1 = im.vb[2 * (y1 - 1)] + im.vb[2 * (y1 - 1) + 1];
   const int row_elems = ow * 3;
-  // horizontal pass: source rows [r0, r1) → tmp (u8)
-  const int nh = (r1 - r0) * row_elems;
-  for (int idx = threadIdx.x; idx < nh; idx += blockDim.x) {
-    const int rr = idx / row_elems;
-    const int rem = idx - rr * row_elems;
-    const int xx = rem / 3;
-    const int c = rem - xx * 3;
+  // horizontal pass: source rows [r0, r1) → tmp [row][x][c] (u8)
+  for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
     const int xmin = im.hb[2 * xx];
     const int n = im.hb[2 * xx + 1];
     const int* k = im.hk + xx * im.ksh;
-    const uint8_t* s = im.src + (int64_t)(r0 + rr) * im.stride + xmin * 3 + c;
-    int acc = 1 << (kPrecisionBits - 1);
-    for (int j = 0; j < n; ++j) acc += (int)s[j * 3] * k[j];
-    tmp[idx] = (uint8_t)clip8(acc);
+    const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
+    uint8_t* t = tmp + xx * 3;
+#pragma unroll 4
+    for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
+      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+      for (int j = 0; j < n; ++j) {
+        const int kj = k[j];
+        a0 += (int)s[3 * j] * kj;
+        a1 += (int)s[3 * j + 1] * kj;
+        a2 += (int)s[3 * j + 2] * kj;
+      }
+      t[0] = (uint8_t)clip8(a0);
+      t[1] = (uint8_t)clip8(a1);
+      t[2] = (uint8_t)clip8(a2);
+    }
   }
   __syncthreads();
-  // vertical pass + rescale + CHW store
-  const int rows = y1 - y0;
-  const int nv = 3 * rows * ow;
+  // vertical pass + rescale + CHW store (coalesced along x in each plane)
   const int64_t plane = (int64_t)oh * ow;
-  for (int idx = threadIdx.x; idx < nv; idx += blockDim.x) {
-    const int c = idx / (rows * ow);
-    const int rem = idx - c * rows * ow;
-    const int yl = rem / ow;
-    const int xx = rem - yl * ow;
-    const int yy = y0 + yl;
-    const int ymin = im.vb[2 * yy] - r0;
-    const int n = im.vb[2 * yy + 1];
-    const int* k = im.vk + yy * im.ksv;
-    int acc = 1 << (kPrecisionBits - 1);
-    for (int j = 0; j < n; ++j) acc += (int)tmp[((ymin + j) * ow + xx) * 3 + c] * k[j];
-    const int v = clip8(acc);
-    im.out[c * plane + (int64_t)yy * ow + xx] = (float)((double)v * (1.0 / 255.0));
+  for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
+    float* o = im.out + (int64_t)y0 * ow + xx;
+#pragma unroll 4
+    for (int yy = y0; yy < y1; ++yy, o += ow) {
+      const int ymin = im.vb[2 * yy] - r0;
+      const int n = im.vb[2 * yy + 1];
+      const int* k = im.vk + yy * im.ksv;
+      const uint8_t* t = tmp + ymin * row_elems + xx * 3;
+      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+      for (int j = 0; j < n; ++j, t += row_elems) {
+        const int kj = k[j];
+        a0 += (int)t[0] * kj;
+        a1 += (int)t[1] * kj;
+        a2 += (int)t[2] * kj;
+      }
+      o[0] = lut[clip8(a0)];
+      o[plane] = lut[clip8(a1)];
+      o[2 * plane] = lut[clip8(a2)];
+    }
   }
 }
 
@@ -226,6 +242,12 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       int T = band_rows(*vc, out_h, out_w * 3, &ntiles);
       SP_ARG_CHECK(T > 0, "sp_preprocess_u8: %dx%d -> %dx%d needs more LDS than available",
                    im.height, im.width, out_h, out_w);
+      // shorter bands when the batch is small, so the launch still spreads over ~2k workgroups
+      const int cap = std::max(4, (out_h * cnt + 2047) / 2048);
+      if (T > cap) {
+        T = cap;
+        ntiles = (out_h + T - 1) / T;
+      }
       PreImg& p = a.img[i];
       p.src = im.data;
       p.h = im.height;

@@ -19,6 +19,9 @@ namespace {
 constexpr int kThreads = 1024;
 constexpr int kMaxN = 36864;  // 144 KiB of keys: covers S = 33,600 at 1280² (LDS 160 KiB)
 constexpr int kMaxK = 512;
+constexpr int kHist = 4;  // histogram copies (LDS: keys 144 KiB + 4 KiB + candidates 4 KiB)
+constexpr int kRedGroups = 16;  // class groups per wave step of the coalesced max-over-classes
+constexpr int kScrG4 = 32;      // max float4 per group there (reduce_c <= 128)
 
 __device__ __forceinline__ uint32_t f2key(float f) {
   uint32_t u = __float_as_uint(f);
@@ -34,7 +37,7 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
                                                          float* __restrict__ vals,
                                                          int32_t* __restrict__ idx_out) {
   __shared__ uint32_t keys[kMaxN];
-  __shared__ uint32_t hist[256];
+  __shared__ uint32_t hist[kHist][256];  // privatised per wave group: sigmoid/logit keys share few top bytes
   __shared__ unsigned long long cand[kMaxK];
   __shared__ uint32_t s_sel[4];  // prefix, remaining, count_gt, count_eq
   __shared__ uint32_t wave_tot[kThreads / 64];
@@ -42,7 +45,37 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
   const int tid = threadIdx.x;
   const int64_t row = blockIdx.x;
   const float* xr = x + row * ldx;
-  for (int i = tid; i < n; i += kThreads) {
+  const int G4 = reduce_c / 4;
+  const bool coalesced = reduce_c > 1 && reduce_c % 4 == 0 && G4 <= kScrG4 && ldx % 4 == 0 &&
+                         ((uintptr_t)x & 15) == 0 && n <= kMaxN - (kThreads / 64) * kRedGroups * kScrG4;
+  if (coalesced) {
+    // max over each group of reduce_c classes with lane-contiguous 16-byte loads: a wave reads kRedGroups
+    // groups at a time, folds each float4 to one partial max in a per-wave LDS scratch (the unused tail of
+    // keys[]), then kRedGroups lanes finish their group's max (order-independent) and store its key.
+    const int w = tid >> 6, ln = tid & 63;
+    float* scr = reinterpret_cast<float*>(keys + kMaxN - (kThreads / 64 - w) * kRedGroups * kScrG4);
+    const float4* xr4 = reinterpret_cast<const float4*>(xr);
+    for (int g0 = w * kRedGroups; g0 < n; g0 += kThreads / 64 * kRedGroups) {
+      const int nf = min(kRedGroups, n - g0) * G4;
+      for (int f = ln; f < nf; f += 64) {
+        const float4 q = xr4[(int64_t)g0 * G4 + f];
+        scr[f] = fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ln < kRedGroups && g0 + ln < n) {
+        float v = scr[ln * G4];
+        for (int j = 1; j < G4; ++j) v = fmaxf(v, scr[ln * G4 + j]);
+        if (apply_sigmoid) v = sigmoidf_(v);
+        keys[g0 + ln] = f2key(v);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+  for (int i = tid; i < n && !coalesced; i += kThreads) {
     float v;
     if (reduce_c > 1) {
       const float* p = xr + (int64_t)i * reduce_c;
@@ -59,21 +92,28 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
   __syncthreads();
 
   uint32_t mask = 0;
+  uint32_t* my_hist = hist[(tid >> 6) % kHist];
   for (int shift = 24; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += kThreads) hist[i] = 0;
+    for (int i = tid; i < kHist * 256; i += kThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t prefix = s_sel[0];
     for (int i = tid; i < n; i += kThreads) {
       const uint32_t key = keys[i];
-      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+      if ((key & mask) == prefix) atomicAdd(&my_hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t tot = 0;
+      for (int j = 0; j < kHist; ++j) tot += hist[j][tid];
+      hist[0][tid] = tot;
     }
     __syncthreads();
     if (tid == 0) {
       uint32_t rem = s_sel[1], cum = 0;
       int bsel = 0;
       for (int bin = 255; bin >= 0; --bin) {
-        if (cum + hist[bin] >= rem) { bsel = bin; break; }
-        cum += hist[bin];
+        if (cum + hist[0][bin] >= rem) { bsel = bin; break; }
+        cum += hist[0][bin];
       }
       s_sel[0] = prefix | ((uint32_t)bsel << shift);
       s_sel[1] = rem - cum;

@@ -172,9 +172,19 @@ class Engine:
             return w.to(torch.bfloat16).view(torch.int16).contiguous()
         return ops.split_bf16x3(w)
 
+    def _pick(self, mode: str, cout: int, kdim: int, small_m: bool = False) -> str:
+        """Per-layer GEMM mode. Under precision "fp32" both operand modes are fp32-accurate, so layers
+        where the plain fp32 MFMA measured faster than the 6-MFMA split (tools/conv_bench.py,
+        profiles/r1/conv_detail_*.json) take it: thin outputs (Cout <= 64: stem, stage-1), thin
+        reductions (K <= 64) and the decoder's M = B·300 linears."""
+        if mode == "x3" and self.precision == "fp32" and (cout <= 64 or kdim <= 64 or small_m):
+            return "f32"
+        return mode
+
     def _mk_conv(self, wk, ci, co, k, sc, sh):
         w = _t(wk, self.dev)
-        return ConvW(w, ci, co, k, _t(sc, self.dev), _t(sh, self.dev), self._wq(w, self._conv_mode))
+        return ConvW(w, ci, co, k, _t(sc, self.dev), _t(sh, self.dev),
+                     self._wq(w, self._pick(self._conv_mode, co, ci * k * k)))
 
     def _conv(self, p, conv_key, bn_pre, frozen):
         w = p[conv_key]
@@ -182,13 +192,15 @@ class Engine:
         sc, sh = (frozen_bn_affine if frozen else eval_bn_affine)(p, bn_pre)
         return self._mk_conv(conv_khwc(w), ci, co, k, sc, sh)
 
-    def _lin(self, p, pre, *more):
+    def _lin(self, p, pre, *more, per_query: bool = False):
+        """per_query: a decoder-side linear over the B·Q selected queries (small M)."""
         ws = [p[pre + ".weight"]] + [p[m + ".weight"] for m in more]
         bs = [p[pre + ".bias"]] + [p[m + ".bias"] for m in more]
         w = np.ascontiguousarray(np.concatenate(ws, 0))
         b = np.concatenate(bs, 0)
         wd = _t(w, self.dev)
-        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(wd, self._lin_mode))
+        mode = self._pick(self._lin_mode, w.shape[0], w.shape[1], small_m=per_query and w.shape[0] > 128)
+        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(wd, mode))
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -235,8 +247,8 @@ class Engine:
         self.enc_output = self._lin(p, "model.enc_output.0")
         self.enc_ln = self._ln(p, "model.enc_output.1")
         self.enc_score = self._lin(p, "model.enc_score_head")
-        self.enc_bbox = [self._lin(p, f"model.enc_bbox_head.layers.{i}") for i in range(3)]
-        self.qpos = [self._lin(p, f"model.decoder.query_pos_head.layers.{i}") for i in range(2)]
+        self.enc_bbox = [self._lin(p, f"model.enc_bbox_head.layers.{i}", per_query=True) for i in range(3)]
+        self.qpos = [self._lin(p, f"model.decoder.query_pos_head.layers.{i}", per_query=True) for i in range(2)]
         D = "model.decoder.layers"
         L = cfg.decoder_layers
         self.value_all = self._lin(p, f"{D}.0.encoder_attn.value_proj",
@@ -244,18 +256,19 @@ class Engine:
         self.dec = []
         for j in range(L):
             q = f"{D}.{j}"
+            pq = {"per_query": True}
             self.dec.append({
-                "qk": self._lin(p, q + ".self_attn.q_proj", q + ".self_attn.k_proj"),
-                "v": self._lin(p, q + ".self_attn.v_proj"),
-                "o": self._lin(p, q + ".self_attn.o_proj"),
+                "qk": self._lin(p, q + ".self_attn.q_proj", q + ".self_attn.k_proj", **pq),
+                "v": self._lin(p, q + ".self_attn.v_proj", **pq),
+                "o": self._lin(p, q + ".self_attn.o_proj", **pq),
                 "ln1": self._ln(p, q + ".self_attn_layer_norm"),
-                "offaw": self._lin(p, q + ".encoder_attn.sampling_offsets", q + ".encoder_attn.attention_weights"),
-                "out": self._lin(p, q + ".encoder_attn.output_proj"),
+                "offaw": self._lin(p, q + ".encoder_attn.sampling_offsets", q + ".encoder_attn.attention_weights", **pq),
+                "out": self._lin(p, q + ".encoder_attn.output_proj", **pq),
                 "ln2": self._ln(p, q + ".encoder_attn_layer_norm"),
-                "fc1": self._lin(p, q + ".mlp.fc1"),
-                "fc2": self._lin(p, q + ".mlp.fc2"),
+                "fc1": self._lin(p, q + ".mlp.fc1", **pq),
+                "fc2": self._lin(p, q + ".mlp.fc2", **pq),
                 "ln3": self._ln(p, q + ".final_layer_norm"),
-                "bbox": [self._lin(p, f"model.decoder.bbox_embed.{j}.layers.{i}") for i in range(3)],
+                "bbox": [self._lin(p, f"model.decoder.bbox_embed.{j}.layers.{i}", **pq) for i in range(3)],
             })
         self.cls_last = self._lin(p, f"model.decoder.class_embed.{L - 1}")
 

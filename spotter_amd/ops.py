@@ -137,7 +137,7 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     nbytes = 4 * (n * h * w * cin * (2 if a2 is not None else 1) + cout * k * k * cin + m * cout
                   * (1 + (res1 is not None) + (res2 is not None)))
     _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
-            (m, cout, k * k * cin, k, stride))
+            (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision]))
     return ho, wo
 
 

@@ -110,7 +110,7 @@ def _bf16(a):
     return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
 
 
-MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16"]
+MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "24"]
 
 
 @pytest.mark.parametrize("case", CONV_CASES[:7] + [(1, 5, 7, 256, 96, 3, 1, "relu")])
@@ -313,8 +313,10 @@ def test_attention(dev, n, heads, dh):
     np.testing.assert_allclose(out.cpu().numpy().reshape(B * n, D), ref, rtol=1e-4, atol=1e-5)
 
 
-def test_msda_matches_oracle(dev):
-    """MSDA core incl. out-of-range sampling points (zero padding) vs oracle.grid_sample_bilinear."""
+@pytest.mark.parametrize("pad", [0, 1])
+def test_msda_matches_oracle(dev, pad):
+    """MSDA core incl. out-of-range sampling points (zero padding) vs oracle.grid_sample_bilinear.
+    pad=0: the decoder's 16-byte-aligned layout (vectorised kernel); pad=1: odd row stride (scalar kernel)."""
     from oracle.rtdetr_np import grid_sample_bilinear
     from spotter_amd import ops
     from spotter_amd.ops import V
@@ -325,12 +327,12 @@ def test_msda_matches_oracle(dev):
     starts = [0, 192, 240]
     S = 252
     D = nH * dh
-    value = rng.standard_normal((B, S, 2 * D)).astype(np.float32)  # two "layers" side by side
+    value = rng.standard_normal((B, S, 2 * D + pad)).astype(np.float32)  # two "layers" side by side
     offaw = np.concatenate([rng.standard_normal((B * Q, nH * nL * nP * 2)) * 2.0,
                             rng.standard_normal((B * Q, nH * nL * nP))], 1).astype(np.float32)
     ref = np.concatenate([rng.uniform(0.05, 0.95, (B * Q, 2)), rng.uniform(0.05, 0.6, (B * Q, 2))], 1).astype(np.float32)
     out = torch.empty(B * Q * D, device=dev)
-    ops.msda(V(T(value.reshape(-1), dev), 0, 2 * D), D, V(T(offaw.reshape(-1), dev), 0, offaw.shape[1]),
+    ops.msda(V(T(value.reshape(-1), dev), 0, 2 * D + pad), D + pad, V(T(offaw.reshape(-1), dev), 0, offaw.shape[1]),
              T(ref, dev), V(out, 0, D), B, S, Q, nH, dh, shapes, starts, nP, 0.5)
     # oracle (M2:200-215 + core M2:44-115)
     off = offaw[:, :nH * nL * nP * 2].reshape(B, Q, nH, nL * nP, 2)
@@ -339,7 +341,7 @@ def test_msda_matches_oracle(dev):
     aw = aw / aw.sum(-1, keepdims=True)
     r = ref.reshape(B, Q, 4)
     loc = r[:, :, None, None, :2] + off * np.float32(1 / nP) * r[:, :, None, None, 2:] * np.float32(0.5)
-    vv = value[:, :, D:].reshape(B, S, nH, dh)
+    vv = value[:, :, D + pad:].reshape(B, S, nH, dh)
     exp = np.zeros((B, nH, Q, dh))
     for l, (h, w) in enumerate(shapes):
         vl = vv[:, starts[l]:starts[l] + h * w].reshape(B, h, w, nH, dh).transpose(0, 3, 1, 2, 4).reshape(B * nH, h, w, dh)
