@@ -120,7 +120,9 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
 // then the fused epilogue on float4s of one output row, with the res1 loads of G consecutive
 // tasks issued before their stores so the residual fetch latency overlaps. NB = TM when the
 // region fits in the operand stages' LDS, else 1 (band by band).
-template <int TM, int TN, int NB>
+// L16: the f32x16 of each 32×32 block holds 2×2 blocks of v_mfma_f32_16x16x32 results (element
+// q = 8·bi + 4·bj + reg; lane l holds rows 16bi + 4(l >> 4) + reg, column 16bj + (l & 15)).
+template <int TM, int TN, int NB, bool L16 = false>
 __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, f32x16 (*acc)[TN],
                                               int64_t mb, int nb, int lane) {
   static_assert(TM % NB == 0, "bands per round must divide TM");
@@ -140,8 +142,11 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int q = 0; q < 16; ++q)
-          region[(i * 32 + (q & 3) + 8 * (q >> 2) + 4 * h) * WN + j * 32 + r] = acc[i0 + i][j][q];
+        for (int q = 0; q < 16; ++q) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          region[(i * 32 + rr) * WN + j * 32 + cc] = acc[i0 + i][j][q];
+        }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
     const int64_t mr = mb + i0 * 32;

@@ -32,6 +32,10 @@
 
 #include "conv_common.h"
 
+#ifndef SP_ABLATE
+#define SP_ABLATE 0
+#endif
+
 namespace sp {
 
 namespace {
@@ -75,6 +79,23 @@ __device__ __forceinline__ f32x16 mfma_planes(const bf16x8* a, const bf16x8* b, 
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  }
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Same six-product sum on v_mfma_f32_16x16x32_bf16 (one 16×16 block, k = 32 per instruction).
+template <int PL>
+__device__ __forceinline__ f32x4 mfma16x16_planes(const bf16x8* a, const bf16x8* b, f32x4 acc) {
+  if constexpr (PL == 1) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
+  } else {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
   }
 }
 
@@ -358,13 +379,17 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
       : "memory");
 }
 
-template <int WM, int WN, int TM, int TN, int PL, int NS>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
+  static_assert(BK == 32 || BK == 16, "k per stage");
+  static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 32 * TM * WM;
   constexpr int BN = 32 * TN * WN;
-  constexpr int CA = BM * 8;  // 16-byte chunks of the fp32 A tile (32 k per row)
-  constexpr int CB = BN * 4;  // 16-byte chunks of one bf16 B plane (32 k per row)
+  constexpr int RA = BK / 4;  // 16-byte chunks per fp32 A row (8 at BK = 32, 4 at BK = 16)
+  constexpr int RB = BK / 8;  // 16-byte chunks per bf16 B row (4 / 2)
+  constexpr int CA = BM * RA;  // 16-byte chunks of the fp32 A tile
+  constexpr int CB = BN * RB;  // 16-byte chunks of one bf16 B plane
   constexpr int GA = CA / NT;
   constexpr int GB = CB / NT;
   static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
@@ -373,7 +398,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
   constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
   constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
   constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
-  static_assert(NS >= 2 && NS <= 4, "stages");
+  static_assert(NS >= 2 && NS <= 6, "stages");
   __shared__ uint4 smem[SMEM];
 
   const sp_conv_desc& d = p.d;
@@ -391,14 +416,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
   const int n0 = (wg - mt * tilesN) * BN;
   const int64_t m0 = (int64_t)mt * BM;
 
-  // A pieces: piece j of this thread covers tile row (j·NT + tid) / 8, LDS position tid % 8,
-  // global chunk (tid % 8) ^ ((row >> 1) & 7) — the same for every j since NT / 8 ≡ 0 (mod 16).
-  const int ca = (tid & 7) ^ (((tid >> 3) >> 1) & 7);
+  // A pieces: piece j of this thread covers tile row (j·NT + tid) / RA, LDS position tid % RA,
+  // global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of the
+  // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
+  // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
+  const int ca = BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
   int a_iy0[GA], a_ix0[GA];
   const float* a_ptr[GA];
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
-    const int64_t m = m0 + ((j * NT + tid) >> 3);
+    const int64_t m = m0 + (j * NT + tid) / RA;
     const bool ok = m < p.M;
     const int64_t mm = ok ? m : 0;
     const int b = (int)(mm / p.HoWo);
@@ -409,25 +436,26 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
     a_ix0[j] = ox * d.stride - d.pad;
     a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
   }
-  // B pieces: row (j·NT + tid) / 4, global chunk (tid % 4) ^ ((row >> 2) & 3) (NT / 4 ≡ 0 mod 16).
-  const int cbk = (tid & 3) ^ (((tid >> 2) >> 2) & 3);
+  // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
+  // (sw16), (row >> 3) & 1 at BK = 16.
+  const int cbk = BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
   const uint16_t* b_ptr[GB];
   bool b_ok[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
-    const int n = n0 + ((j * NT + tid) >> 2);
+    const int n = n0 + (j * NT + tid) / RB;
     b_ok[j] = n < d.Cout;
     b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
   }
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
 
   int s_kh = 0, s_kw = 0, s_c0 = 0;
-  const int nk_all = p.K / KT;
+  const int nk_all = p.K / BK;
   const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
   const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
   const int nk = kt1 - kt0;
   {
-    const int k0 = kt0 * KT;
+    const int k0 = kt0 * BK;
     const int tap = k0 / d.Cin;
     s_c0 = k0 - tap * d.Cin;
     s_kh = tap / d.KW;
@@ -446,7 +474,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
       const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
       glds16(src, st + j * NT * 16);
     }
-    const int k0 = kt * KT;
+    const int k0 = kt * BK;
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl)
 #pragma unroll
@@ -455,7 +483,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
                                   : static_cast<const void*>(zero + cbk * 16);
         glds16(src, st + (CA + pl * CB + j * NT) * 16);
       }
-    s_c0 += KT;
+    s_c0 += BK;
     if (s_c0 >= d.Cin) {
       s_c0 = 0;
       if (++s_kw == d.KW) {
@@ -478,27 +506,78 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
 
+  // M16: each 32×32 block of the wave as 2×2 blocks of v_mfma_f32_16x16x32_bf16 (lane l: A row l & 15,
+  // B column l & 15, k = 8(l >> 4) + j; C rows 4(l >> 4) + reg, column l & 15) on the same LDS images.
+  f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
+  if constexpr (M16) {
+#pragma unroll
+    for (int i = 0; i < 2 * TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
   auto compute = [&](int buf) {
     const uint4* st = smem + buf * STAGE;
+    if constexpr (M16) {
+      const int c16 = lane & 15, g = lane >> 4;
+      bf16x8 fb[2 * TN][PL];
 #pragma unroll
-    for (int s = 0; s < KT / 16; ++s) {
-      bf16x8 fb[TN][PL];
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < 2 * TN; ++j) {
+        const int brow = wn * TN * 32 + j * 16 + c16;
 #pragma unroll
         for (int pl = 0; pl < PL; ++pl)
-          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(wn * TN * 32 + j * 32 + r, 2 * s + h));
+          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(brow, g));
+      }
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 32 + i * 32 + r;
+      for (int i = 0; i < 2 * TM; ++i) {
+        const int row = wm * TM * 32 + i * 16 + c16;
         const int sz = (row >> 1) & 7;
-        const int c0 = 4 * s + 2 * h;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * 8 + (c0 ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * 8 + ((c0 + 1) ^ sz));
+        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
+        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
         bf16x8 fa[PL];
         split_frag<PL>(x0, x1, fa);
 #pragma unroll
+        for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
+      }
+      return;
+    }
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      bf16x8 fb[TN][PL];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int brow = wn * TN * 32 + j * 32 + r;
+        const int bpos = BK == 32 ? sw16(brow, 2 * s + h) : brow * 2 + (h ^ ((brow >> 3) & 1));
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * TM * 32 + i * 32 + r;
+        const int sz = BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
+        const int c0 = 4 * s + 2 * h;
+        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
+        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
+        bf16x8 fa[PL];
+#if SP_ABLATE == 2  // no split: one cvt, planes aliased (same MFMA count)
+        {
+          bf16x8 hh;
+          hh[0] = (__bf16)x0.x; hh[1] = (__bf16)x0.y; hh[2] = (__bf16)x0.z; hh[3] = (__bf16)x0.w;
+          hh[4] = (__bf16)x1.x; hh[5] = (__bf16)x1.y; hh[6] = (__bf16)x1.z; hh[7] = (__bf16)x1.w;
+          for (int q = 0; q < PL; ++q) fa[q] = hh;
+        }
+#else
+        split_frag<PL>(x0, x1, fa);
+#endif
+#if SP_ABLATE == 3  // no MFMA: keep the operands alive
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          for (int q = 0; q < PL; ++q) asm volatile("" ::"v"(fa[q]), "v"(fb[j][q]));
+#else
+#pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa, fb[j], acc[i][j]);
+#endif
       }
     }
   };
@@ -510,29 +589,42 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
   for (int kt = 0; kt < nk; ++kt) {
     // retire stage kt: stages kt+1 .. min(kt+NS-2, nk-1) may stay in flight
     const int ahead = (nk - 1 - kt) < (NS - 2) ? (nk - 1 - kt) : (NS - 2);
-    if constexpr (NS >= 4) {
-      if (ahead >= 2) wait_vmcnt<2 * GLDS>();
-      else if (ahead == 1) wait_vmcnt<GLDS>();
-      else wait_vmcnt<0>();
-    } else if constexpr (NS == 3) {
-      if (ahead >= 1) wait_vmcnt<GLDS>();
-      else wait_vmcnt<0>();
-    } else {
-      wait_vmcnt<0>();
-    }
+    if (NS >= 6 && ahead >= 4) wait_vmcnt<(NS >= 6 ? 4 * GLDS : 0)>();
+    else if (NS >= 5 && ahead >= 3) wait_vmcnt<(NS >= 5 ? 3 * GLDS : 0)>();
+    else if (NS >= 4 && ahead >= 2) wait_vmcnt<(NS >= 4 ? 2 * GLDS : 0)>();
+    else if (NS >= 3 && ahead >= 1) wait_vmcnt<(NS >= 3 ? GLDS : 0)>();
+    else wait_vmcnt<0>();
     raw_barrier();
-    if (kt + NS - 1 < nk) issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
+#if SP_ABLATE == 1  // no DMA in the loop (compute on stale stages)
+    if (false)
+#else
+    if (kt + NS - 1 < nk)
+#endif
+      issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
     compute(kt % NS);
   }
 
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
-                            lane);
+  if constexpr (M16) {
+    // 16×16 blocks → the f32x16 of their 32×32 block: element q = 8·bi + 4·bj + reg
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = acc4[2 * i + (q >> 3)][2 * j + ((q >> 2) & 1)][q & 3];
+  }
+  epilogue_tile<TM, TN, NB, M16>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
+                                 n0 + wn * TN * 32, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int NS>
+template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
 int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
+  if (a.d.Cin % BK || a.K % BK) {
+    set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
+    return -1;
+  }
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
   const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
   if (tiles > 0x7fffffff) {
@@ -541,9 +633,9 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -787,6 +879,225 @@ int launch_pipe(const ConvArgs& a, int planes, hipStream_t s) {
   return launch_splitk_reduce(a, s);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Ping-pong LDS-DMA kernel: 8 waves as two groups of four (waves 0-3 = group A, 4-7 = group B; a
+// workgroup's waves land on the 4 SIMDs in turn, so every SIMD holds one wave of each group). Per
+// k-tile a wave runs a MEMORY phase (fragment ds_reads + the fp32→bf16-plane split, and for group A
+// the LDS-DMA issue of the next k-tile) and a COMPUTE phase (its TM·TN·(PL==3 ? 6 : 1)·2 MFMAs),
+// each ended by a workgroup barrier. Group B starts one phase late, so on every SIMD one wave's
+// MFMA chain runs while the other wave does its loads and split VALU: the matrix pipe no longer
+// waits for the operand work (the glds kernel measured that work and the MFMAs as additive).
+// Phase p: A does MEM(p/2) on even p and COMP on odd p; B does MEM on odd and COMP on even p > 0.
+// Stages: 2 LDS buffers; group A issues k-tile t+1 during MEM(t) into the buffer k-tile t-1 used
+// (group B finished reading it in phase 2t-1), and waits for it (vmcnt 0) at the end of COMP(t),
+// before the barrier that opens phase 2t+2 where A first reads it.
+template <int TM, int TN, int PL>
+__global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
+  constexpr int WM = 4, WN = 2;
+  constexpr int NT = 512, NL = 256;  // threads, loader threads (group A)
+  constexpr int BM = 32 * TM * WM;
+  constexpr int BN = 32 * TN * WN;
+  constexpr int CA = BM * 8;  // 16-byte chunks of the fp32 A tile (32 k per row)
+  constexpr int CB = BN * 4;  // 16-byte chunks of one bf16 B plane
+  constexpr int GA = CA / NL;
+  constexpr int GB = CB / NL;
+  static_assert(GA * NL == CA && GB * NL == CB && GB >= 1, "DMA pieces must tile the loader group");
+  constexpr int STAGE = CA + PL * CB;
+  constexpr int NS = 2;
+  constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
+  constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
+  constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
+  static_assert(SMEM * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[SMEM];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const bool grpA = wave < 4;
+
+  const int tilesN = (d.Cout + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = wg / tilesN;
+  const int n0 = (wg - mt * tilesN) * BN;
+  const int64_t m0 = (int64_t)mt * BM;
+
+  // loader state (group A threads only use it)
+  const int lt = tid & (NL - 1);
+  const int ca = (lt & 7) ^ (((lt >> 3) >> 1) & 7);
+  int a_iy0[GA], a_ix0[GA];
+  const float* a_ptr[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int64_t m = m0 + ((j * NL + lt) >> 3);
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int b = (int)(mm / p.HoWo);
+    const int rem = (int)(mm - (int64_t)b * p.HoWo);
+    const int oy = rem / d.Wo;
+    const int ox = rem - oy * d.Wo;
+    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
+    a_ix0[j] = ox * d.stride - d.pad;
+    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+  }
+  const int cbk = (lt & 3) ^ (((lt >> 2) >> 2) & 3);
+  const uint16_t* b_ptr[GB];
+  bool b_ok[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int n = n0 + ((j * NL + lt) >> 2);
+    b_ok[j] = n < d.Cout;
+    b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
+  }
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+
+  int s_kh = 0, s_kw = 0, s_c0 = 0;
+  const int nk_all = p.K / KT;
+  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
+  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
+  const int nk = kt1 - kt0;
+  {
+    const int k0 = kt0 * KT;
+    const int tap = k0 / d.Cin;
+    s_c0 = k0 - tap * d.Cin;
+    s_kh = tap / d.KW;
+    s_kw = tap - s_kh * d.KW;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane((wave & 3) * 64 * 16);
+  auto issue = [&](int kt, int buf) {  // group A only
+    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
+      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
+      glds16(src, st + j * NL * 16);
+    }
+    const int k0 = kt * KT;
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl)
+#pragma unroll
+      for (int j = 0; j < GB; ++j) {
+        const void* src = b_ok[j] ? static_cast<const void*>(b_ptr[j] + pl * wps + k0)
+                                  : static_cast<const void*>(zero + cbk * 16);
+        glds16(src, st + (CA + pl * CB + j * NL) * 16);
+      }
+    s_c0 += KT;
+    if (s_c0 >= d.Cin) {
+      s_c0 = 0;
+      if (++s_kw == d.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+  };
+
+  const int wm = wave / WN;
+  const int wn = wave - wm * WN;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  int a_row[TM], a_sz[TM], b_row[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    a_row[i] = (wm * TM * 32 + i * 32 + r) * 8;
+    a_sz[i] = ((wm * TM * 32 + i * 32 + r) >> 1) & 7;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) b_row[j] = wn * TN * 32 + j * 32 + r;
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+
+  bf16x8 fa[2][TM][PL], fb[2][TN][PL];
+  auto mem = [&](int buf) {  // fragments of both k16 steps of stage buffer `buf`
+    const uint4* st = smem + buf * STAGE;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fb[s][j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(b_row[j], 2 * s + h));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int c0 = 4 * s + 2 * h;
+        const float4 x0 = *reinterpret_cast<const float4*>(st + a_row[i] + (c0 ^ a_sz[i]));
+        const float4 x1 = *reinterpret_cast<const float4*>(st + a_row[i] + ((c0 + 1) ^ a_sz[i]));
+        split8<PL>(x0, x1, fa[s][i]);
+      }
+    }
+  };
+  auto comp = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa[s][i], fb[s][j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: k-tile 0 landed and visible before anyone's first MEM phase
+  if (grpA && nk > 0) {
+    issue(kt0, 0);
+    wait_vmcnt<0>();
+  }
+  barrier();
+  if (!grpA) barrier();  // group B runs one phase behind
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    // MEM(t)
+    if (grpA && t + 1 < nk) issue(kt0 + t + 1, buf ^ 1);
+    mem(buf);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this phase's LDS reads are done before the buffer is refilled
+    barrier();
+    // COMP(t)
+    comp();
+    if (grpA) wait_vmcnt<0>();  // k-tile t+1 landed before the barrier that opens A's MEM(t+1)
+    barrier();
+  }
+  if (grpA) barrier();  // match group B's extra barrier
+
+  __syncthreads();
+  float* smemf = reinterpret_cast<float*>(smem);
+  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+                            lane);
+}
+
+template <int TM, int TN>
+int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
+  constexpr int BM = 32 * TM * 4, BN = 32 * TN * 2;
+  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  dim3 grid((unsigned)tiles, 1, a.splits);
+  if (planes == 3)
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 3>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 1>), grid, dim3(512), 0, s, a);
+  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 ping-pong)" : "sp_conv2d(bf16 ping-pong)");
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
+}
+
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
@@ -823,6 +1134,12 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
+  if (cfg >= 31 && cfg <= 32 && !a.d.A2) {
+    switch (cfg) {
+      case 31: return launch_pp<2, 2>(a, planes, s);  // 256×128, waves of 64×64
+      default: return launch_pp<1, 2>(a, planes, s);  // 128×128, waves of 32×64
+    }
+  }
   if (cfg >= 21 && cfg <= 26 && !a.d.A2) {
     switch (cfg) {
       case 21: return launch_pipe<2, 2, 2, 2, 4>(a, planes, s);   // 128×128, 4 stages
@@ -833,7 +1150,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (cfg >= 11 && cfg <= 20 && !a.d.A2) {
+  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 43)) && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
       case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
@@ -844,17 +1161,29 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       case 18: return launch_glds<2, 2, 2, 4, 2>(a, planes, s);  // 128×256, 4 waves of 64×128
       case 19: return launch_glds<2, 1, 2, 4, 2>(a, planes, s);  // 128×128, 2 waves of 64×128, 2 stages
       case 20: return launch_glds<2, 1, 2, 4, 3>(a, planes, s);  // 128×128, 2 waves of 64×128
+      case 33: return launch_glds<4, 2, 2, 4, 2>(a, planes, s);  // 256×256, 8 waves of 64×128
+      case 34: return launch_glds<2, 4, 4, 2, 2>(a, planes, s);  // 256×256, 8 waves of 128×64
+      case 35: return launch_glds<4, 1, 2, 4, 4, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 4 stages
+      case 36: return launch_glds<4, 1, 2, 4, 5, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 5 stages
+      case 37: return launch_glds<4, 2, 2, 4, 3, 16>(a, planes, s);  // 256×256, k16 stages × 3
+      case 38: return launch_glds<4, 2, 2, 4, 4, 16>(a, planes, s);  // 256×256, k16 stages × 4
+      case 41: return launch_glds<4, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 12 on 16x16x32 MFMAs
+      case 42: return launch_glds<4, 2, 2, 4, 2, 32, true>(a, planes, s);  // cfg 33 on 16x16x32 MFMAs
+      case 43: return launch_glds<2, 2, 2, 2, 3, 32, true>(a, planes, s);  // cfg 11 on 16x16x32 MFMAs
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || cfg > 26 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || cfg > 43 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
-    // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64.
+    // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
+    // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes
+    // half of its second column of tiles, and at K = 256 the 256×128 tile stays ahead).
     const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };
     const bool dma = !a.d.A2;
     if (a.splits > 1) cfg = 4;
     else if (a.d.Cout <= 64) cfg = dma ? (tiles(128, 64) >= 192 ? 16 : 14) : 4;
-    else if (tiles(256, 128) >= 192) cfg = dma ? 12 : 2;
+    else if (dma && a.d.Cout % 256 == 0 && a.K >= 512 && tiles(256, 256) >= 192) cfg = 33;
+    else if (tiles(256, 128) >= 192) cfg = dma ? (a.M >= 150000 ? 41 : 12) : 2;  // tall M: 16x16x32 +6 %
     else if (tiles(64, 128) >= 192) cfg = dma ? 13 : 3;
     else cfg = dma ? 14 : 4;
     if (cfg >= 11) return launch_mfma16(a, planes, cfg, s);
