@@ -1,7 +1,7 @@
 // Small fused multi-head self-attention (AIFI: 400 tokens × 8 heads × 48 at
 // 640²; decoder: 300 queries × 8 heads × 32). softmax(Q Kᵀ · scale) V with an
-// online (running max / sum) softmax, one query per lane, K/V tiles of 64 keys
-// broadcast from LDS. Restates eager_attention_forward / sdpa (M2:245-270) as
+// online (running max / sum) softmax corrected once per block of 16 keys, one query
+// per lane, K/V tiles of 64 keys broadcast from LDS. Restates eager_attention_forward / sdpa (M2:245-270) as
 // called by RTDetrV2SelfAttention (M2:300-336); Q/K/V/O projections run on the
 // MFMA GEMM (conv_gemm.hip). ≈1 % of the step's FLOPs, VALU-bound.
 #include "common.h"
@@ -33,6 +33,8 @@ __global__ __launch_bounds__(64) void attn_kernel(const float* __restrict__ q, i
     qv[c] = t.x; qv[c + 1] = t.y; qv[c + 2] = t.z; qv[c + 3] = t.w;
     acc[c] = acc[c + 1] = acc[c + 2] = acc[c + 3] = 0.f;
   }
+  // online softmax per block of SB keys: one running-max correction per block instead of per key
+  constexpr int SB = 16;
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < n; k0 += KT) {
     const int nk = min(KT, n - k0);
@@ -46,31 +48,46 @@ __global__ __launch_bounds__(64) void attn_kernel(const float* __restrict__ q, i
           *reinterpret_cast<const float4*>(v + (rowbase + k0 + r) * ldv + hh * DH + c);
     }
     __syncthreads();
-    for (int j = 0; j < nk; ++j) {
-      const float* kr = Ks + j * DH;
-      float s = 0.f;
+    for (int j0 = 0; j0 < nk; j0 += SB) {
+      float sc[SB];
+      float mt = -INFINITY;
 #pragma unroll
-      for (int c = 0; c < DH; c += 4) {
-        float4 t = *reinterpret_cast<const float4*>(kr + c);
-        s = fmaf(qv[c], t.x, s);
-        s = fmaf(qv[c + 1], t.y, s);
-        s = fmaf(qv[c + 2], t.z, s);
-        s = fmaf(qv[c + 3], t.w, s);
+      for (int jj = 0; jj < SB; ++jj) {
+        const float* kr = Ks + (j0 + jj) * DH;
+        float s = 0.f;
+#pragma unroll
+        for (int c = 0; c < DH; c += 4) {
+          float4 t = *reinterpret_cast<const float4*>(kr + c);
+          s = fmaf(qv[c], t.x, s);
+          s = fmaf(qv[c + 1], t.y, s);
+          s = fmaf(qv[c + 2], t.z, s);
+          s = fmaf(qv[c + 3], t.w, s);
+        }
+        s *= scale;
+        sc[jj] = (j0 + jj < nk) ? s : -INFINITY;
+        mt = fmaxf(mt, sc[jj]);
       }
-      s *= scale;
-      const float mn = fmaxf(m, s);
-      const float corr = expf(m - mn);
-      const float p = expf(s - mn);
-      l = l * corr + p;
-      m = mn;
-      const float* vr = Vs + j * DH;
+      const float mn = fmaxf(m, mt);
+      const float corr = expf(m - mn);  // m = -inf on the first block: corr = 0, acc / l are 0
+      l *= corr;
 #pragma unroll
-      for (int c = 0; c < DH; c += 4) {
-        float4 t = *reinterpret_cast<const float4*>(vr + c);
-        acc[c] = fmaf(p, t.x, acc[c] * corr);
-        acc[c + 1] = fmaf(p, t.y, acc[c + 1] * corr);
-        acc[c + 2] = fmaf(p, t.z, acc[c + 2] * corr);
-        acc[c + 3] = fmaf(p, t.w, acc[c + 3] * corr);
+      for (int c = 0; c < DH; ++c) acc[c] *= corr;
+      m = mn;
+#pragma unroll
+      for (int jj = 0; jj < SB; ++jj) {
+        if (j0 + jj < nk) {  // wave-uniform; rows past nk hold stale LDS
+          const float pj = expf(sc[jj] - mn);
+          l += pj;
+          const float* vr = Vs + (j0 + jj) * DH;
+#pragma unroll
+          for (int c = 0; c < DH; c += 4) {
+            float4 t = *reinterpret_cast<const float4*>(vr + c);
+            acc[c] = fmaf(pj, t.x, acc[c]);
+            acc[c + 1] = fmaf(pj, t.y, acc[c + 1]);
+            acc[c + 2] = fmaf(pj, t.z, acc[c + 2]);
+            acc[c + 3] = fmaf(pj, t.w, acc[c + 3]);
+          }
+        }
       }
     }
   }

@@ -20,8 +20,6 @@ constexpr int kThreads = 1024;
 constexpr int kMaxN = 36864;  // 144 KiB of keys: covers S = 33,600 at 1280² (LDS 160 KiB)
 constexpr int kMaxK = 512;
 constexpr int kHist = 4;  // histogram copies (LDS: keys 144 KiB + 4 KiB + candidates 4 KiB)
-constexpr int kRedGroups = 16;  // class groups per wave step of the coalesced max-over-classes
-constexpr int kScrG4 = 32;      // max float4 per group there (reduce_c <= 128)
 
 __device__ __forceinline__ uint32_t f2key(float f) {
   uint32_t u = __float_as_uint(f);
@@ -46,33 +44,41 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
   const int64_t row = blockIdx.x;
   const float* xr = x + row * ldx;
   const int G4 = reduce_c / 4;
-  const bool coalesced = reduce_c > 1 && reduce_c % 4 == 0 && G4 <= kScrG4 && ldx % 4 == 0 &&
-                         ((uintptr_t)x & 15) == 0 && n <= kMaxN - (kThreads / 64) * kRedGroups * kScrG4;
+  const bool coalesced = reduce_c > 1 && reduce_c % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
   if (coalesced) {
-    // max over each group of reduce_c classes with lane-contiguous 16-byte loads: a wave reads kRedGroups
-    // groups at a time, folds each float4 to one partial max in a per-wave LDS scratch (the unused tail of
-    // keys[]), then kRedGroups lanes finish their group's max (order-independent) and store its key.
-    const int w = tid >> 6, ln = tid & 63;
-    float* scr = reinterpret_cast<float*>(keys + kMaxN - (kThreads / 64 - w) * kRedGroups * kScrG4);
+    // max over each group of reduce_c classes: a wave covers 16 groups per step, lane (part p = l >> 4,
+    // group g = l & 15) loading float4s p, p+4, p+8, ... of group g — every wave-instruction reads
+    // 16 × 64 contiguous bytes — then two xor-shuffles fold the 4 parts (max is order-independent).
+    // Two steps are in flight per iteration.
+    const int w = tid >> 6, ln = tid & 63, g = ln & 15, part = ln >> 4;
     const float4* xr4 = reinterpret_cast<const float4*>(xr);
-    for (int g0 = w * kRedGroups; g0 < n; g0 += kThreads / 64 * kRedGroups) {
-      const int nf = min(kRedGroups, n - g0) * G4;
-      for (int f = ln; f < nf; f += 64) {
-        const float4 q = xr4[(int64_t)g0 * G4 + f];
-        scr[f] = fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w));
+    constexpr int kW = kThreads / 64;
+    for (int g0 = w * 32; g0 < n; g0 += kW * 32) {
+      float m2[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int grp = g0 + 16 * u + g;
+        float m = -INFINITY;
+        if (grp < n) {
+          const float4* q = xr4 + (int64_t)grp * G4;
+          for (int t = part; t < G4; t += 4) {
+            const float4 v = q[t];
+            m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+          }
+        }
+        m2[u] = m;
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (ln < kRedGroups && g0 + ln < n) {
-        float v = scr[ln * G4];
-        for (int j = 1; j < G4; ++j) v = fmaxf(v, scr[ln * G4 + j]);
-        if (apply_sigmoid) v = sigmoidf_(v);
-        keys[g0 + ln] = f2key(v);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float m = m2[u];
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int grp = g0 + 16 * u + g;
+        if (part == 0 && grp < n) {
+          if (apply_sigmoid) m = sigmoidf_(m);
+          keys[grp] = f2key(m);
+        }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
   for (int i = tid; i < n && !coalesced; i += kThreads) {

@@ -222,8 +222,11 @@ def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q
     for i, ((h, w), s0) in enumerate(zip(shapes, starts)):
         d.level_h[i], d.level_w[i], d.level_start[i] = h, w, s0
     d.offset_scale = offset_scale
-    # compulsory: the value maps once, offsets + weights + reference boxes per query, the output
-    nbytes = 4 * (B * S * heads * head_dim + B * Q * (heads * L * points * 3 + 4 + heads * head_dim))
+    # compulsory: the value rows the samples can touch — the whole value map, or, when the map is
+    # larger than the 4 bilinear corners of every sample (1280²: 34.4 MB vs 14.7 MB per image), the
+    # corner rows — plus offsets + weights + reference boxes per query and the output
+    value_bytes = min(S, Q * L * points * 4) * heads * head_dim
+    nbytes = 4 * (B * value_bytes + B * Q * (heads * L * points * 3 + 4 + heads * head_dim))
     # per sample: 4 bilinear taps (multiply-add) + the attention weight
     flops = B * Q * heads * L * points * head_dim * 10
     _launch("msda", "sp_msda", (C.byref(d), stream()), flops, nbytes, (B, S, Q, heads, head_dim, L, points))
