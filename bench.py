@@ -56,7 +56,7 @@ def parse():
 # kernel class -> (bound, peak, unit); peaks from MI355X_MICROARCH.md (dense, no sparsity)
 CLASS_BOUND = {
     "conv": ("mfma", None, "TFLOP/s"),  # fp32 or bf16 MFMA peak by --precision
-    "attention": ("valu", 157.3, "TFLOP/s"),  # AIFI online-softmax attention, fp32 FMA on VALU
+    "attention": ("mfma", 157.3, "TFLOP/s"),  # flash-style attention on v_mfma_f32_16x16x4_f32 (fp32 peak)
     "msda": ("hbm", HBM_PEAK_GBS, "GB/s"),
     "preprocess": ("hbm", HBM_PEAK_GBS, "GB/s"),
     "topk": ("hbm", HBM_PEAK_GBS, "GB/s"),

@@ -1,109 +1,131 @@
-// Small fused multi-head self-attention (AIFI: 400 tokens × 8 heads × 48 at
-// 640²; decoder: 300 queries × 8 heads × 32). softmax(Q Kᵀ · scale) V with an
-// online (running max / sum) softmax corrected once per block of 16 keys, one query
-// per lane, K/V tiles of 64 keys broadcast from LDS. Restates eager_attention_forward / sdpa (M2:245-270) as
-// called by RTDetrV2SelfAttention (M2:300-336); Q/K/V/O projections run on the
-// MFMA GEMM (conv_gemm.hip). ≈1 % of the step's FLOPs, VALU-bound.
+// Small fused multi-head self-attention (AIFI: 400 tokens × 8 heads × 48 at 640², 1600 at 1280²;
+// decoder: 300 queries × 8 heads × 32): softmax(Q Kᵀ · scale) V. Restates eager_attention_forward /
+// sdpa (M2:245-270) as called by RTDetrV2SelfAttention (M2:300-336); the Q/K/V/O projections run on
+// the MFMA GEMM (conv_gemm.hip).
+//
+// Flash-style on the fp32 matrix core (v_mfma_f32_16x16x4_f32: exact fp32 fmaf chains, as the
+// GEMMs). One wave owns 16 queries of one (image, head); a 4-wave workgroup shares 64-key K/V tiles
+// in LDS. Per 16-key block the wave computes the transposed scores Sᵀ = K Qᵀ (lane l: keys
+// 4(l>>4)+i, query l&15), so the online softmax over keys reduces over 4 registers plus two
+// cross-group shuffles, and the probabilities are already the B operand of Oᵀ += Vᵀ P: MFMA step s
+// pairs lane group g with key 4g+s on both operands (the k order of an MFMA is free), no transpose
+// through LDS. Oᵀ lands as 4 consecutive head channels of one query per lane → float4 stores.
 #include "common.h"
 
 namespace sp {
 namespace {
 
-constexpr int KT = 64;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int KT = 64;  // keys per LDS tile
 
 template <int DH>
-__global__ __launch_bounds__(64) void attn_kernel(const float* __restrict__ q, int64_t ldq,
-                                                  const float* __restrict__ k, int64_t ldk,
-                                                  const float* __restrict__ v, int64_t ldv,
-                                                  float* __restrict__ o, int64_t ldo, int n,
-                                                  float scale) {
-  __shared__ __attribute__((aligned(16))) float Ks[KT * DH];
-  __shared__ __attribute__((aligned(16))) float Vs[KT * DH];
-  const int lane = threadIdx.x;
+__global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict__ q, int64_t ldq,
+                                                        const float* __restrict__ k, int64_t ldk,
+                                                        const float* __restrict__ v, int64_t ldv,
+                                                        float* __restrict__ o, int64_t ldo, int n,
+                                                        float scale) {
+  static_assert(DH % 16 == 0, "head dim in 16-channel blocks");
+  constexpr int LD = DH + 4;     // padded LDS row (floats): 16 key rows → distinct bank groups
+  constexpr int QS = DH / 4;     // S MFMA steps (k = 4 channels each)
+  constexpr int DB = DH / 16;    // 16-channel output blocks
+  __shared__ __attribute__((aligned(16))) float Ks[KT * LD];
+  __shared__ __attribute__((aligned(16))) float Vs[KT * LD];
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int c16 = lane & 15;
+  const int g = lane >> 4;
   const int b = blockIdx.z;
   const int hh = blockIdx.y;
-  const int qi = blockIdx.x * 64 + lane;
-  const bool valid = qi < n;
   const int64_t rowbase = (int64_t)b * n;
-  float qv[DH], acc[DH];
-  const float* qr = q + (rowbase + (valid ? qi : 0)) * ldq + hh * DH;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+  const int qi = q0 + c16;
+  // B operand of Sᵀ = K Qᵀ: step s, lane group g supplies channel g·QS + s of query qi.
+  float qv[QS];
+  {
+    const float* qr = q + (rowbase + (qi < n ? qi : n - 1)) * ldq + hh * DH + g * QS;
 #pragma unroll
-  for (int c = 0; c < DH; c += 4) {
-    float4 t = *reinterpret_cast<const float4*>(qr + c);
-    qv[c] = t.x; qv[c + 1] = t.y; qv[c + 2] = t.z; qv[c + 3] = t.w;
-    acc[c] = acc[c + 1] = acc[c + 2] = acc[c + 3] = 0.f;
+    for (int c = 0; c < QS; c += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(qr + c);
+      qv[c] = t.x; qv[c + 1] = t.y; qv[c + 2] = t.z; qv[c + 3] = t.w;
+    }
   }
-  // online softmax per block of SB keys: one running-max correction per block instead of per key
-  constexpr int SB = 16;
+  f32x4 acc[DB];
+#pragma unroll
+  for (int d = 0; d < DB; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
   for (int k0 = 0; k0 < n; k0 += KT) {
     const int nk = min(KT, n - k0);
     __syncthreads();
-    for (int idx = lane; idx < nk * (DH / 4); idx += 64) {
+    for (int idx = tid; idx < KT * (DH / 4); idx += 256) {
       const int r = idx / (DH / 4);
       const int c = (idx - r * (DH / 4)) * 4;
-      *reinterpret_cast<float4*>(Ks + r * DH + c) =
-          *reinterpret_cast<const float4*>(k + (rowbase + k0 + r) * ldk + hh * DH + c);
-      *reinterpret_cast<float4*>(Vs + r * DH + c) =
-          *reinterpret_cast<const float4*>(v + (rowbase + k0 + r) * ldv + hh * DH + c);
+      float4 kk = make_float4(0.f, 0.f, 0.f, 0.f), vv = kk;  // rows past nk: zeros (0·p, never NaN)
+      if (r < nk) {
+        kk = *reinterpret_cast<const float4*>(k + (rowbase + k0 + r) * ldk + hh * DH + c);
+        vv = *reinterpret_cast<const float4*>(v + (rowbase + k0 + r) * ldv + hh * DH + c);
+      }
+      *reinterpret_cast<float4*>(Ks + r * LD + c) = kk;
+      *reinterpret_cast<float4*>(Vs + r * LD + c) = vv;
     }
     __syncthreads();
-    for (int j0 = 0; j0 < nk; j0 += SB) {
-      float sc[SB];
+    for (int j0 = 0; j0 < nk; j0 += 16) {
+      // Sᵀ block: A = K[key j0 + c16][channel g·QS + s]
+      f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* kr = Ks + (j0 + c16) * LD + g * QS;
+#pragma unroll
+      for (int c = 0; c < QS; c += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(kr + c);
+        st = __builtin_amdgcn_mfma_f32_16x16x4f32(t.x, qv[c], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_16x16x4f32(t.y, qv[c + 1], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_16x16x4f32(t.z, qv[c + 2], st, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_16x16x4f32(t.w, qv[c + 3], st, 0, 0, 0);
+      }
+      // lane holds scores of keys j0 + 4g + i for query qi
       float mt = -INFINITY;
 #pragma unroll
-      for (int jj = 0; jj < SB; ++jj) {
-        const float* kr = Ks + (j0 + jj) * DH;
-        float s = 0.f;
-#pragma unroll
-        for (int c = 0; c < DH; c += 4) {
-          float4 t = *reinterpret_cast<const float4*>(kr + c);
-          s = fmaf(qv[c], t.x, s);
-          s = fmaf(qv[c + 1], t.y, s);
-          s = fmaf(qv[c + 2], t.z, s);
-          s = fmaf(qv[c + 3], t.w, s);
-        }
-        s *= scale;
-        sc[jj] = (j0 + jj < nk) ? s : -INFINITY;
-        mt = fmaxf(mt, sc[jj]);
+      for (int i = 0; i < 4; ++i) {
+        st[i] = (j0 + 4 * g + i < nk) ? st[i] * scale : -INFINITY;
+        mt = fmaxf(mt, st[i]);
       }
+      mt = fmaxf(mt, __shfl_xor(mt, 16));
+      mt = fmaxf(mt, __shfl_xor(mt, 32));
       const float mn = fmaxf(m, mt);
-      const float corr = expf(m - mn);  // m = -inf on the first block: corr = 0, acc / l are 0
-      l *= corr;
-#pragma unroll
-      for (int c = 0; c < DH; ++c) acc[c] *= corr;
+      const float corr = expf(m - mn);  // first block: m = -inf → 0 (acc, l are 0)
       m = mn;
+      float pr[4];
 #pragma unroll
-      for (int jj = 0; jj < SB; ++jj) {
-        if (j0 + jj < nk) {  // wave-uniform; rows past nk hold stale LDS
-          const float pj = expf(sc[jj] - mn);
-          l += pj;
-          const float* vr = Vs + (j0 + jj) * DH;
+      for (int i = 0; i < 4; ++i) pr[i] = expf(st[i] - mn);
+      l = l * corr + ((pr[0] + pr[1]) + (pr[2] + pr[3]));
 #pragma unroll
-          for (int c = 0; c < DH; c += 4) {
-            float4 t = *reinterpret_cast<const float4*>(vr + c);
-            acc[c] = fmaf(pj, t.x, acc[c]);
-            acc[c + 1] = fmaf(pj, t.y, acc[c + 1]);
-            acc[c + 2] = fmaf(pj, t.z, acc[c + 2]);
-            acc[c + 3] = fmaf(pj, t.w, acc[c + 3]);
-          }
-        }
+      for (int d = 0; d < DB; ++d) acc[d] *= corr;
+      // Oᵀ[channel][query] += Σ_s V[key j0 + 4g + s][channel] · P[key j0 + 4g + s][query]
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const float* vr = Vs + (j0 + 4 * g + s) * LD + c16;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) acc[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(vr[d * 16], pr[s], acc[d], 0, 0, 0);
       }
     }
   }
-  if (!valid) return;
+  // l: this lane group's partial sum over its keys → total over the 4 groups (same query)
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  if (qi >= n) return;
   const float inv = 1.0f / l;
-  float* orow = o + (rowbase + qi) * ldo + hh * DH;
+  float* orow = o + (rowbase + qi) * ldo + hh * DH + 4 * g;
 #pragma unroll
-  for (int c = 0; c < DH; c += 4)
-    *reinterpret_cast<float4*>(orow + c) = make_float4(acc[c] * inv, acc[c + 1] * inv, acc[c + 2] * inv, acc[c + 3] * inv);
+  for (int d = 0; d < DB; ++d)
+    *reinterpret_cast<float4*>(orow + d * 16) =
+        make_float4(acc[d][0] * inv, acc[d][1] * inv, acc[d][2] * inv, acc[d][3] * inv);
 }
 
 template <int DH>
 int launch(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
            float* o, int64_t ldo, int batch, int n, int heads, float scale, hipStream_t s) {
   dim3 grid((n + 63) / 64, heads, batch);
-  hipLaunchKernelGGL((attn_kernel<DH>), grid, dim3(64), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n, scale);
+  hipLaunchKernelGGL((attn_mfma_kernel<DH>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n, scale);
   return check_launch("sp_attention");
 }
 

@@ -34,10 +34,14 @@ constexpr int BK = 32;
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 2); }
 
 
-template <int TM, int TN, int DB>
+// WM × WN waves (WM·WN = 4), each a (32·TM) × (32·TN) patch: 2×2 is the square default, 4×1 gives
+// the 32- and 64-wide N tiles that thin outputs (Cout = 32 / 64: stem, stage 1) need without idle MFMAs.
+template <int TM, int TN, int DB, int WM = 2>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
-  constexpr int BM = 64 * TM;
-  constexpr int BN = 64 * TN;
+  constexpr int WN = 4 / WM;
+  static_assert(WM * WN == 4, "four waves per workgroup");
+  constexpr int BM = 32 * WM * TM;
+  constexpr int BN = 32 * WN * TN;
   constexpr int PA = BM / 32;  // loader passes (32 rows per pass)
   constexpr int PB = BN / 32;
   constexpr int STAGE = (BM + BN) * BK;
@@ -141,8 +145,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
 
   const int wave = tid >> 6;
   const int lane = tid & 63;
-  const int wm = wave >> 1;
-  const int wn = wave & 1;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
   const int r = lane & 31;
   const int h = lane >> 5;
 
@@ -242,11 +246,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
   }
 }
 
-template <int TM, int TN, int DB>
+template <int TM, int TN, int DB, int WM = 2>
 int launch(const ConvArgs& a, hipStream_t s) {
-  constexpr int BM = 64 * TM, BN = 64 * TN;
+  constexpr int BM = 32 * WM * TM, BN = 32 * (4 / WM) * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM), a.splits);
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM>), grid, dim3(256), 0, s, a);
   int rc = check_launch("sp_conv2d");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -344,11 +348,22 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     case 121: return launch<1, 2, 1>(a, s);
     case 110: return launch<1, 1, 0>(a, s);
     case 111: return launch<1, 1, 1>(a, s);
+    // 4×1 wave grids: "4<TM><TN><DB>" → tile (128·TM) × (32·TN)
+    case 4110: return launch<1, 1, 0, 4>(a, s);
+    case 4111: return launch<1, 1, 1, 4>(a, s);
+    case 4210: return launch<2, 1, 0, 4>(a, s);
+    case 4211: return launch<2, 1, 1, 4>(a, s);
+    case 4120: return launch<1, 2, 0, 4>(a, s);
+    case 4121: return launch<1, 2, 1, 4>(a, s);
     default: break;
   }
   // Tile choice (measured on MI355X, tools/conv_bench.py): the kernel is latency-bound, so
   // occupancy beats operand reuse except for long-K, wide-N, tall-M convs.
   const int64_t tiles64 = ((a.M + 63) / 64) * ((d->Cout + 63) / 64);
+  // Cout <= 32 (stem): the 4×1 wave grid's 128×32 tile, no idle N half (1.69× on the stem 3×3,
+  // 1.23× on the Cin = 3 stem conv; gpurun_out/s5 → profiles/r1/conv_bench_thin_fp32.jsonl).
+  if (d->Cout <= 32) return launch<1, 1, 0, 4>(a, s);
+  if (d->Cout <= 64 && a.M >= 500000 && a.K >= 288) return launch<2, 1, 0>(a, s);
   if (a.K >= 3000 && d->Cout >= 384 && a.M >= 100000) return launch<2, 2, 0>(a, s);
   if (a.K <= 128 || d->Cout <= 64 || tiles64 < 3000) return launch<1, 1, 0>(a, s);
   return launch<1, 2, 0>(a, s);

@@ -89,11 +89,13 @@ def test_conv2d_matches_oracle(dev, case, workspace=None):
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("cfg", ["220", "221", "210", "211", "120", "121", "110", "111"])
+@pytest.mark.parametrize("cfg", ["220", "221", "210", "211", "120", "121", "110", "111",
+                                 "4110", "4111", "4210", "4211", "4120", "4121"])
 def test_conv2d_every_tile_config(dev, cfg, monkeypatch):
     """Each tile variant (SP_CONV_CFG override) on a ragged 3×3 and a 1×1 with residuals."""
     monkeypatch.setenv("SP_CONV_CFG", cfg)
-    for case in [(2, 11, 9, 64, 136, 3, 1, "silu"), (1, 7, 13, 96, 72, 1, 1, "relu"), (1, 9, 9, 3, 32, 3, 2, None)]:
+    for case in [(2, 11, 9, 64, 136, 3, 1, "silu"), (1, 7, 13, 96, 72, 1, 1, "relu"), (1, 9, 9, 3, 32, 3, 2, None),
+                 (2, 13, 11, 32, 32, 3, 1, "relu")]:
         test_conv2d_matches_oracle(dev, case)
 
 
@@ -290,7 +292,8 @@ def test_layernorm(dev, d):
     np.testing.assert_allclose(y.cpu().numpy().reshape(77, d), ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("n,heads,dh", [(300, 8, 32), (400, 8, 48), (70, 2, 64)])
+@pytest.mark.parametrize("n,heads,dh", [(300, 8, 32), (400, 8, 48), (70, 2, 64), (1, 1, 32), (17, 3, 48),
+                                        (1600, 8, 48), (129, 2, 32)])
 def test_attention(dev, n, heads, dh):
     from spotter_amd import ops
     from spotter_amd.ops import V

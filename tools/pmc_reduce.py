@@ -16,9 +16,9 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce")), ("msda", ("msda",)), ("attention", ("attn_kernel",)),
+CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce")), ("msda", ("msda",)), ("attention", ("attn_",)),
            ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)), ("layernorm", ("layernorm",))]
-LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_kernel", "preprocess": None, "topk": "topk",
+LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_", "preprocess": None, "topk": "topk",
            "layernorm": "layernorm"}
 
 

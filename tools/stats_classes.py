@@ -9,7 +9,7 @@ import json
 import sys
 
 CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
-           ("attention", ("attn_kernel",)), ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)),
+           ("attention", ("attn_",)), ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)),
            ("layernorm", ("layernorm",)), ("postprocess_decode", ("decode_kernel",))]
 
 
