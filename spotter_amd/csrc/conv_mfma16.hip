@@ -1150,7 +1150,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 48)) && !a.d.A2) {
+  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51)) && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
       case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
@@ -1175,10 +1175,13 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       case 45: return launch_glds<2, 2, 2, 2, 2>(a, planes, s);      // 128×128, k32 × 2 stages
       case 46: return launch_glds<2, 2, 2, 2, 2, 16>(a, planes, s);  // 128×128, k16 × 2 stages
       case 48: return launch_glds<2, 2, 2, 4, 2, 16>(a, planes, s);  // 128×256, 4 waves of 64×128, k16 × 2
+      // 64-wide N (Cout = 64 layers): 4 waves of 64×64 stacked along M
+      case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
+      case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || cfg > 48 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || cfg > 51 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes
@@ -1194,7 +1197,8 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     else if (dma && x3 && a.K <= 256 && a.d.Cout >= 512 && tiles(128, 128) >= 192) cfg = 46;
     else if (dma && x3 && a.d.Cout % 128 == 0 && a.d.Cout % 256 != 0 && a.M >= 40000 &&
              (a.M < 150000 || a.d.Cout == 128) && tiles(128, 128) >= 192) cfg = 45;
-    else if (a.d.Cout <= 64) cfg = dma ? (tiles(128, 64) >= 192 ? 16 : 14) : 4;
+    else if (a.d.Cout <= 64)
+      cfg = dma ? (x3 && a.d.Cout == 64 && tiles(256, 64) >= 192 ? 51 : (tiles(128, 64) >= 192 ? 16 : 14)) : 4;
     else if (dma && a.d.Cout % 256 == 0 && a.K >= 512 && tiles(256, 256) >= 192) cfg = 33;
     else if (tiles(256, 128) >= 192) cfg = dma ? (a.M >= 150000 ? 41 : 12) : 2;  // tall M: 16x16x32 +6 %
     else if (tiles(64, 128) >= 192) cfg = dma ? 13 : 3;

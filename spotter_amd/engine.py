@@ -178,6 +178,8 @@ class Engine:
         profiles/r1/conv_detail_*.json) take it: thin outputs (Cout <= 64: stem, stage-1), thin
         reductions (K <= 64) and the decoder's M = B·300 linears."""
         if mode == "x3" and self.precision == "fp32" and (cout <= 64 or kdim <= 64 or small_m):
+            if cout == 64 and kdim >= 576 and not small_m:
+                return mode  # 3×3 64→64 (stage 1): the split kernel's 256×64 tile, 1.09× (conv_bench_thin_x3)
             return "f32"
         return mode
 
