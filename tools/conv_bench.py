@@ -36,6 +36,9 @@ SHAPES = [
     (1, 1, 9600, 256, 256, 1, 1, None, True, 32),       # 14 decoder linear          0.8
     (32, 640, 640, 3, 32, 3, 2, "relu", False, 1),      # 15 stem conv1 (Cin=3)
     (32, 160, 160, 64, 256, 1, 1, "relu", True, 4),     # 16 stage0 expand
+    (32, 20, 20, 384, 384, 3, 1, None, False, 3),       # 17 CCFM 3x3 @20²
+    (32, 20, 20, 512, 2048, 1, 1, "relu", True, 3),     # 18 stage4 expand
+    (32, 80, 80, 512, 128, 1, 1, "relu", False, 3),     # 19 stage1 reduce
 ]
 
 
