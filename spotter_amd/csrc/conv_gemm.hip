@@ -30,6 +30,11 @@ namespace sp {
 namespace {
 
 constexpr int BK = 32;
+// Split-K target for long-K GEMMs on mid-size grids (bs1 /detect path: the CCFM 3×3 at M = 6400 ran
+// 300 workgroups × 108 k-tiles; split 2 takes it from 213 to 143 µs).
+#ifndef SP_SPLITK_BLOCKS
+#define SP_SPLITK_BLOCKS 1024
+#endif
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chunk ^ ((row >> 1) & 7)) << 2); }
 
@@ -328,9 +333,14 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   {
     const int64_t blocks64 = ((a.M + 63) / 64) * ((d->Cout + 63) / 64);
     const int nk = (a.K + BK - 1) / BK;
-    if (d->workspace && blocks64 < 256 && nk >= 16) {
-      int sp = (int)((512 + blocks64 - 1) / blocks64);
-      if (sp > nk / 8) sp = nk / 8;
+    // measured at bs1 (profiles/r1/bs1_detail_*.json): short grids split to ~512 workgroups with
+    // ≥ 8 k-tiles each; tiny-M linears (< 64 tiles) split even at K = 256; grids of up to
+    // SP_SPLITK_BLOCKS tiles split only when each workgroup would walk ≥ 64 k-tiles.
+    int sp = 1;
+    if (blocks64 < 64 && nk >= 8 && nk < 16) sp = nk / 4;
+    else if (blocks64 < 256 && nk >= 16) sp = (int)((512 + blocks64 - 1) / blocks64), sp = sp < nk / 8 ? sp : nk / 8;
+    else if (blocks64 < SP_SPLITK_BLOCKS && nk >= 64) sp = (int)((SP_SPLITK_BLOCKS + blocks64 - 1) / blocks64);
+    if (d->workspace && sp > 1) {
       if (sp > 16) sp = 16;
       while (sp > 1 && (int64_t)sp * a.M * a.ldp > d->workspace_elems) --sp;
       if (sp > 1) a.splits = sp;

@@ -322,7 +322,7 @@ class Engine:
         return c
 
     # ------------------------------------------------------------------ layers
-    SPLITK_ELEMS = 4 << 20  # 16 MB fp32 split-K scratch per context
+    SPLITK_ELEMS = 16 << 20  # 64 MB fp32 split-K scratch per context
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2

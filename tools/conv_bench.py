@@ -39,10 +39,15 @@ SHAPES = [
     (32, 20, 20, 384, 384, 3, 1, None, False, 3),       # 17 CCFM 3x3 @20²
     (32, 20, 20, 512, 2048, 1, 1, "relu", True, 3),     # 18 stage4 expand
     (32, 80, 80, 512, 128, 1, 1, "relu", False, 3),     # 19 stage1 reduce
+    # bs1 /detect latency path (run with --ws: the engine hands every conv a split-K workspace)
+    (1, 80, 80, 384, 384, 3, 1, None, False, 3),        # 20 CCFM 3x3 @80² bs1
+    (1, 40, 40, 256, 256, 3, 1, "relu", False, 22),     # 21 stage3 3x3 bs1
+    (1, 40, 40, 1024, 256, 1, 1, "relu", False, 22),    # 22 stage3 reduce bs1
+    (1, 40, 40, 256, 1024, 1, 1, "relu", True, 23),     # 23 stage3 expand bs1
 ]
 
 
-def bench_one(dev, shape, prec, cfg, reps):
+def bench_one(dev, shape, prec, cfg, reps, ws=False):
     n, h, w, cin, cout, k, st, act, resid, _ = shape
     if cfg and cfg != "-":
         os.environ["SP_CONV_CFG"] = cfg
@@ -63,6 +68,9 @@ def bench_one(dev, shape, prec, cfg, reps):
         kw["wt16"] = wt.to(torch.bfloat16).view(torch.int16).contiguous()
     elif prec == "f32x3":
         kw["wt_planes"] = ops.split_bf16x3(wt)
+
+    if ws:
+        kw["workspace"] = torch.empty(16 << 20, device=dev)
 
     def run():
         ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, st, pad, view(out, cout), scale=sc, shift=sh,
@@ -89,6 +97,7 @@ def main():
     ap.add_argument("--cfgs", default="-")
     ap.add_argument("--shapes", default=None)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--ws", action="store_true", help="pass a split-K workspace (as the engine does)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     which = [int(i) for i in a.shapes.split(",")] if a.shapes else range(len(SHAPES))
@@ -97,7 +106,7 @@ def main():
         for prec in a.prec.split(","):
             for cfg in a.cfgs.split(","):
                 try:
-                    r = bench_one(dev, SHAPES[si], prec, cfg, a.reps)
+                    r = bench_one(dev, SHAPES[si], prec, cfg, a.reps, a.ws)
                 except RuntimeError as e:  # a tile config the shape/mode cannot use (e.g. LDS overflow)
                     print(json.dumps({"shape": SHAPES[si][:7], "prec": prec, "cfg": cfg, "skipped": str(e)}), flush=True)
                     continue
