@@ -7,7 +7,7 @@
  *   processor(images=PIL, return_tensors="pt")           -> sp_preprocess_u8
  *   model(**inputs) (RTDetrV2ForObjectDetection.forward) -> sp_conv2d, sp_maxpool3x3s2,
  *        sp_avgpool2x2_ceil, sp_upsample2x_nearest, sp_layernorm, sp_attention,
- *        sp_msda, sp_topk_rows, sp_gather_rows, sp_ref_init, sp_box_refine
+ *        sp_msda, sp_rowmax, sp_topk_rows, sp_gather_rows, sp_ref_init, sp_box_refine
  *   processor.post_process_object_detection(...)         -> sp_postprocess
  * (HF sources: transformers/models/rt_detr/image_processing_pil_rt_detr.py:
  * 451-462, 508-578; transformers/models/rt_detr_v2/modeling_rt_detr_v2.py:
@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 4
+#define SP_ABI_VERSION 5
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -145,6 +145,10 @@ int sp_msda(const sp_msda_desc* d, void* stream);
  * value descending, ties by lower index. vals may be NULL. Requires k <= 512. */
 int sp_topk_rows(const float* x, int64_t ldx, int rows, int n, int reduce_c, int apply_sigmoid,
                  int k, float* vals, int32_t* idx, void* stream);
+/* out[r] = max_c x[r*ldx + c], c < C: the per-anchor class max in front of query selection
+ * (enc_outputs_class.max(-1).values, M2:1599), spread over the chip; sp_topk_rows(reduce_c = 1)
+ * then ranks one key per anchor. */
+int sp_rowmax(const float* x, int64_t ldx, int64_t rows, int c, float* out, void* stream);
 /* dst[b, i, :] = src[b*src_rows + idx[b, i], :] */
 int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,
                    int batch, int d, float* dst, int64_t ld_dst, void* stream);

@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -72,6 +72,7 @@ _SIGS = {
     "sp_attention": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),
     "sp_msda": (i32, [C.POINTER(SpMsdaDesc), vp]),
     "sp_topk_rows": (i32, [vp, i64, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "sp_rowmax": (i32, [vp, i64, i64, i32, vp, vp]),
     "sp_gather_rows": (i32, [vp, i64, i32, vp, i32, i32, i32, vp, i64, vp]),
     "sp_ref_init": (i32, [vp, i64, vp, vp, i32, i32, vp, vp]),
     "sp_box_refine": (i32, [vp, i64, vp, i32, vp]),

@@ -210,8 +210,55 @@ __global__ __launch_bounds__(512) void decode_kernel(const float* __restrict__ b
   if (threadIdx.x == 0) counts[b] = s_cnt;
 }
 
+// Per-anchor max over the class logits (the reduction in front of query selection's top-k, M2:1599),
+// spread over the whole chip: 4 lanes per row, float4 loads, two xor-shuffles. The top-k kernel then
+// works on one key per anchor instead of streaming the [S, C] logits through a single workgroup.
+__global__ __launch_bounds__(256) void rowmax4_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                      int c4, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = t >> 2;
+  const int part = (int)(t & 3);
+  float m = -INFINITY;
+  if (r < rows) {
+    const float4* q = reinterpret_cast<const float4*>(x + r * ldx);
+    for (int j = part; j < c4; j += 4) {
+      const float4 v = q[j];
+      m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  if (r < rows && part == 0) out[r] = m;
+}
+
+__global__ __launch_bounds__(256) void rowmax_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int c,
+                                                     float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const float* q = x + r * ldx;
+  float m = q[0];
+  for (int j = 1; j < c; ++j) m = fmaxf(m, q[j]);
+  out[r] = m;
+}
+
 }  // namespace
 }  // namespace sp
+
+extern "C" int sp_rowmax(const float* x, int64_t ldx, int64_t rows, int c, float* out, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(x && out && rows > 0 && c > 0 && ldx >= c, "sp_rowmax: bad args");
+  hipStream_t s = as_stream(stream);
+  if (c % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0) {
+    const int64_t g = (rows * 4 + 255) / 256;
+    SP_ARG_CHECK(g <= 0x7fffffff, "sp_rowmax: rows");
+    hipLaunchKernelGGL(rowmax4_kernel, dim3((unsigned)g), dim3(256), 0, s, x, ldx, rows, c / 4, out);
+  } else {
+    const int64_t g = (rows + 255) / 256;
+    SP_ARG_CHECK(g <= 0x7fffffff, "sp_rowmax: rows");
+    hipLaunchKernelGGL(rowmax_kernel, dim3((unsigned)g), dim3(256), 0, s, x, ldx, rows, c, out);
+  }
+  return check_launch("sp_rowmax");
+}
 
 extern "C" int sp_topk_rows(const float* x, int64_t ldx, int rows, int n, int reduce_c, int apply_sigmoid,
                             int k, float* vals, int32_t* idx, void* stream) {

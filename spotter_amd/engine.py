@@ -588,7 +588,9 @@ class Engine:
         ops.layernorm(view(om_pre, D), *self.enc_ln, view(om, D), rows, D, cfg.layer_norm_eps)
         self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
         topk = self._buf("topk", B, Q, dtype=torch.int32)
-        ops.topk_rows(V(cls, 0, S * NC), B, S, Q, topk, reduce_c=NC)
+        cmax = self._buf("enc_cls_max", rows)
+        ops.rowmax(view(cls, NC), rows, NC, cmax)
+        ops.topk_rows(V(cmax, 0, S), B, S, Q, topk)
         Bq = B * Q
         h = self._buf("dec_h", Bq, D)
         ops.gather_rows(view(om, D), S, topk, Q, B, D, view(h, D))

@@ -243,6 +243,13 @@ def topk_rows(x: V, rows, n, k, idx: torch.Tensor, vals: torch.Tensor | None = N
             0, 4 * rows * (n * reduce_c + 2 * k), (rows, n, reduce_c, k))
 
 
+def rowmax(x: V, rows, c, out: torch.Tensor):
+    """out[r] = max over the first c columns of row r (query selection's per-anchor class max)."""
+    assert out.dtype == torch.float32 and out.numel() >= rows
+    _launch("topk", "sp_rowmax", (x.need(rows, c, "rowmax.x"), x.ld, rows, c, out.data_ptr(), stream()),
+            0, 4 * rows * (c + 1), (rows, c))
+
+
 def gather_rows(src: V, src_rows, idx: torch.Tensor, k, batch, d, dst: V):
     sp_ = src.need(batch * src_rows, d, "gather.src")
     dp = dst.need(batch * k, d, "gather.dst")

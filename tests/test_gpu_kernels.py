@@ -434,3 +434,16 @@ def test_preprocess_matches_golden_digests(dev):
         res = torch.empty(3 * o * o, device=dev)
         ops.preprocess_u8([T(img, dev)], res, int(o), int(o))
         assert hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest() == str(dig), (h, w, o)
+
+
+@pytest.mark.parametrize("rows,c,ld", [(1, 80, 80), (8400 * 2, 80, 80), (333, 7, 9), (1000, 12, 16)])
+def test_rowmax(dev, rows, c, ld):
+    """sp_rowmax: per-anchor class max (query selection), vectorised and scalar paths; max is exact."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    rng = np.random.default_rng(rows + c)
+    x = rng.standard_normal((rows, ld)).astype(np.float32)
+    out = torch.empty(rows, device=dev)
+    ops.rowmax(view(T(x.reshape(-1), dev), ld), rows, c, out)
+    np.testing.assert_array_equal(out.cpu().numpy(), x[:, :c].max(1))
