@@ -119,8 +119,14 @@ __device__ __forceinline__ int clip8(int acc) {
 
 // Thread mapping: every pass walks output columns with the threads and rows with a loop, so the
 // per-column coefficients are loaded once and reused down the band (no index divisions).
+// MAXT > 0: every image of the launch has at most MAXT horizontal taps; the column's coefficients sit
+// in registers and all 3·MAXT source bytes of a row are loaded at once (taps past n are predicated
+// off and weigh 0, so the integer sums are unchanged). MAXT = 0: generic tap loop.
+// The u8 band buffer is dynamic LDS sized to the launch's tallest band (a 10-row band of a 640-wide
+// output needs 21 KB, not the 48 KB cap), so more workgroups share a CU and hide the byte-load latency.
+template <int MAXT>
 __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
-  __shared__ uint8_t tmp[kLdsBytes];
+  extern __shared__ uint8_t tmp[];
   __shared__ float lut[256];
   const PreImg& im = a.img[blockIdx.y];
   const int tile = blockIdx.x;
@@ -134,6 +140,31 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
   const int r1 = im.vb[2 * (y1 - 1)] + im.vb[2 * (y1 - 1) + 1];
   const int row_elems = ow * 3;
   // horizontal pass: source rows [r0, r1) → tmp [row][x][c] (u8)
+  if constexpr (MAXT > 0) {
+    for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
+      const int xmin = im.hb[2 * xx];
+      const int n = im.hb[2 * xx + 1];
+      int kr[MAXT];
+#pragma unroll
+      for (int j = 0; j < MAXT; ++j) kr[j] = j < n ? im.hk[xx * im.ksh + j] : 0;
+      const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
+      uint8_t* t = tmp + xx * 3;
+#pragma unroll 8  // 8 source rows of byte loads in flight per thread: the pass is load-latency bound
+      for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
+        int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+#pragma unroll
+        for (int j = 0; j < MAXT; ++j) {
+          const bool ok = j < n;
+          a0 += (ok ? (int)s[3 * j] : 0) * kr[j];
+          a1 += (ok ? (int)s[3 * j + 1] : 0) * kr[j];
+          a2 += (ok ? (int)s[3 * j + 2] : 0) * kr[j];
+        }
+        t[0] = (uint8_t)clip8(a0);
+        t[1] = (uint8_t)clip8(a1);
+        t[2] = (uint8_t)clip8(a2);
+      }
+    }
+  } else
   for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
     const int xmin = im.hb[2 * xx];
     const int n = im.hb[2 * xx + 1];
@@ -227,7 +258,7 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
     a.out_h = out_h;
     a.out_w = out_w;
     int cnt = n - base < kMaxImgs ? n - base : kMaxImgs;
-    int max_tiles = 0;
+    int max_tiles = 0, max_ksh = 0, lds = 0;
     for (int i = 0; i < cnt; ++i) {
       const sp_image_u8& im = images[base + i];
       SP_ARG_CHECK(im.data && im.height > 0 && im.width > 0 && im.row_stride >= 3 * im.width,
@@ -248,6 +279,11 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
         T = cap;
         ntiles = (out_h + T - 1) / T;
       }
+      for (int y0 = 0; y0 < out_h; y0 += T) {  // LDS bytes of this image's tallest band
+        const int y1 = y0 + T < out_h ? y0 + T : out_h;
+        const int rows = vc->h_bounds[2 * (y1 - 1)] + vc->h_bounds[2 * (y1 - 1) + 1] - vc->h_bounds[2 * y0];
+        if (rows * out_w * 3 > lds) lds = rows * out_w * 3;
+      }
       PreImg& p = a.img[i];
       p.src = im.data;
       p.h = im.height;
@@ -263,8 +299,18 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       p.ntiles = ntiles;
       p.out = out + (int64_t)(base + i) * 3 * out_h * out_w;
       if (ntiles > max_tiles) max_tiles = ntiles;
+      if (hc->ksize > max_ksh) max_ksh = hc->ksize;
     }
-    hipLaunchKernelGGL(preprocess_kernel, dim3(max_tiles, cnt), dim3(256), 0, s, a);
+    const dim3 grid(max_tiles, cnt);
+    lds = (lds + 15) & ~15;
+    if (max_ksh <= 3)  // up-scaling and same-size sources
+      hipLaunchKernelGGL(preprocess_kernel<3>, grid, dim3(256), lds, s, a);
+    else if (max_ksh <= 5)
+      hipLaunchKernelGGL(preprocess_kernel<5>, grid, dim3(256), lds, s, a);
+    else if (max_ksh <= 7)  // down-scaling by up to 3x (1920 → 640, 3840 → 1280)
+      hipLaunchKernelGGL(preprocess_kernel<7>, grid, dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL(preprocess_kernel<0>, grid, dim3(256), lds, s, a);
     int rc = check_launch("sp_preprocess_u8");
     if (rc) return rc;
   }
