@@ -56,11 +56,32 @@ def measure(preset="r101vd", iters=200, graphs=True, model=None):
         model(pixel_values=x)
         torch.cuda.synchronize()
         fw.append(time.perf_counter() - t0)
+    # per-stage p50 (each stage synchronised): where the non-forward part of the p50 goes
+    stages = {"decode": [], "processor": [], "model": [], "post_process": []}
+    for _ in range(min(iters, 50)):
+        t0 = time.perf_counter()
+        with Image.open(io.BytesIO(jpeg)) as raw:
+            image = raw.convert("RGB")
+        t1 = time.perf_counter()
+        inputs = proc(images=image, return_tensors="pt").to("cpu")
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        with torch.no_grad():
+            out = model(**inputs)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        det = proc.post_process_object_detection(out, target_sizes=torch.tensor([[image.size[1], image.size[0]]]),
+                                                 threshold=0.5)[0]
+        _ = ([model.config.id2label[int(l.item())] for l in det["labels"]], det["boxes"].tolist())
+        t4 = time.perf_counter()
+        for k, a, b in (("decode", t0, t1), ("processor", t1, t2), ("model", t2, t3), ("post_process", t3, t4)):
+            stages[k].append((b - a) * 1e3)
     ts, fw = np.array(ts) * 1e3, np.array(fw) * 1e3
     return {"metric": "p50 /detect core latency (bs1, 1200x717 JPEG: decode, preprocess, forward, "
                       "post_process, labels/boxes to host)", "graphs": graphs,
             "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
-            "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": iters, "preset": preset}
+            "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": iters, "preset": preset,
+            "stages_p50_ms": {k: round(float(np.percentile(v, 50)), 3) for k, v in stages.items()}}
 
 
 def main():
