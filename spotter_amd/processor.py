@@ -132,7 +132,9 @@ class SpotterImageProcessor:
             work = torch.empty((b, k), dtype=torch.int32, device=dev)
             ops.postprocess(logits.contiguous().float(), boxes.contiguous().float(), tsd, k, float(threshold),
                             scores, labels, bx, counts, work)
-            host = [t.to("cpu") for t in (scores, labels, bx, counts)]
+            # four async copies into pinned host memory, one wait (not four synchronous round trips)
+            host = [t.to("cpu", non_blocking=True) for t in (scores, labels, bx, counts)]
+            torch.cuda.current_stream(dev).synchronize()
         s_h, l_h, b_h, c_h = host
         res = []
         for i in range(b):
