@@ -316,7 +316,8 @@ def main():
         modes = {}
         per_mfma = {"x3": (6, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
                     "bf16": (1, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
-                    "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS)}
+                    "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS),
+                    "direct": (1, "v_fma_f32 (VALU stem conv, no MFMA)", FP32_MFMA_PEAK_TFLOPS)}
         for md, c in rec.conv_modes().items():
             a = c["flops"] / (c["ms"] * 1e-3) / 1e12
             mult, instr, pk = per_mfma[md]

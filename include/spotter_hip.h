@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 5
+#define SP_ABI_VERSION 6
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -125,6 +125,12 @@ int sp_conv2d(const sp_conv_desc* d, void* stream);
 
 /* NCHW → NHWC (pixel_values layout of the processor contract → conv layout). */
 int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* stream);
+/* Backbone stem conv 1 (RN:71-114: 3x3 stride 2 pad 1, Cin 3, FrozenBN affine M2:748-758, ReLU)
+ * read directly from NCHW pixel_values x [n,3,h,w]; wt [cout][27] in (kh, kw, ci) order; y NHWC
+ * [n, (h-1)/2+1, (w-1)/2+1, cout]. Replaces sp_nchw_to_nhwc + sp_conv2d for this layer. cout 32 or 64,
+ * act 0 (none) or 1 (relu). (ABI v6) */
+int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, const float* shift, float* y,
+                           int n, int h, int w, int cout, int act, void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). */
 int sp_maxpool3x3s2(const float* x, float* y, int n, int h, int w, int c, void* stream);
 /* nn.AvgPool2d(2, 2, 0, ceil_mode=True) on NHWC (RN:150, RN:202). */

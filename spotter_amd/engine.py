@@ -334,14 +334,27 @@ class Engine:
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                           row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
-    def backbone(self, px_nhwc: torch.Tensor, B, H, W):
-        """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC)."""
+    def _direct_stem(self) -> bool:
+        """The stem's first conv (Cin 3, K = 27) runs on the direct NCHW kernel (sp_stem_conv3x3s2_nchw)
+        in the fp32-weight modes; the bf16 variants keep it on the GEMM path with their rounding."""
+        c = self.stem[0]
+        return c.cin == 3 and c.k == 3 and c.cout in (32, 64) and c.w16 is None
+
+    def backbone(self, pixel_values: torch.Tensor, B, H, W):
+        """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC).
+        pixel_values is the processor's NCHW batch (IPP:461-462)."""
         e = self.cfg.embedding_size
         h1, w1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
         s0 = self._buf("stem0", B, h1, w1, e // 2)
         s1 = self._buf("stem1", B, h1, w1, e // 2)
         s2 = self._buf("stem2", B, h1, w1, e)
-        self._cv(view(px_nhwc, 3), B, H, W, self.stem[0], 2, view(s0, e // 2), act="relu")
+        c0 = self.stem[0]
+        if self._direct_stem():
+            ops.stem_conv_nchw(pixel_values, c0.w, c0.scale, c0.shift, view(s0, e // 2), c0.cout, act="relu")
+        else:
+            px = self._buf("px_nhwc", B, H, W, 3)
+            ops.nchw_to_nhwc(pixel_values, px)
+            self._cv(view(px, 3), B, H, W, c0, 2, view(s0, e // 2), act="relu")
         self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act="relu")
         self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act="relu")
         h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
@@ -566,9 +579,7 @@ class Engine:
 
     def _run(self, pixel_values, out_logits, out_boxes):
         B, C, H, W = pixel_values.shape
-        px = self._buf("px_nhwc", B, H, W, 3)
-        ops.nchw_to_nhwc(pixel_values, px)
-        feats = yield from self.backbone(px, B, H, W)
+        feats = yield from self.backbone(pixel_values.contiguous(), B, H, W)
         enc = yield from self.encoder(feats, B)
         src, shapes, starts, S = self.decoder_inputs(enc, B)
         yield

@@ -166,6 +166,26 @@ def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):
             8 * x.numel())
 
 
+def stem_conv_nchw(x: torch.Tensor, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V,
+                   cout: int, act=None):
+    """Backbone stem conv 1 (RN:71-114: 3x3/2, Cin 3, FrozenBN, ReLU) from NCHW pixel_values x [n,3,h,w]
+    into NHWC rows y [n*ho*wo, cout] (dense rows: y.ld == cout). Direct VALU kernel, no transpose pass."""
+    n, c, h, w = x.shape
+    if c != 3 or x.dtype != torch.float32 or not x.is_contiguous() or not x.is_cuda:
+        raise ValueError("stem_conv_nchw: x must be a contiguous float32 CUDA tensor [n,3,h,w]")
+    if cout not in (32, 64) or y.ld != cout:
+        raise ValueError("stem_conv_nchw: cout must be 32 or 64 with dense output rows")
+    if wt.numel() != cout * 27 or scale.numel() < cout or shift.numel() < cout:
+        raise ValueError("stem_conv_nchw: weight / affine size mismatch")
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    m = n * ho * wo
+    yp = y.need(m, cout, "stem.y")
+    _launch("conv", "sp_stem_conv3x3s2_nchw",
+            (x.data_ptr(), wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, n, h, w, cout, ACT[act],
+             stream()), 2 * m * cout * 27, 4 * (x.numel() + cout * 27 + m * cout), (m, cout, 27, 3, 2, "direct"))
+    return ho, wo
+
+
 def maxpool3x3s2(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c

@@ -275,6 +275,31 @@ def test_nchw_to_nhwc(dev):
     np.testing.assert_array_equal(y.cpu().numpy().reshape(2, 5, 7, 3), x.transpose(0, 2, 3, 1))
 
 
+@pytest.mark.parametrize("case", [(1, 17, 15, 32, "relu"), (2, 640, 640, 32, "relu"), (3, 33, 8, 64, None),
+                                  (1, 1, 1, 32, "relu")])
+def test_stem_conv_nchw(dev, case):
+    """Direct stem conv (sp_stem_conv3x3s2_nchw) from NCHW pixel_values vs the oracle conv on the
+    NHWC transpose (RN:71-114 first layer: 3x3/2 pad 1, FrozenBN affine, ReLU); odd sizes cover the
+    zero-padded right/bottom edges, 640² the bench shape."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    n, h, w, cout, act = case
+    rng = np.random.default_rng(h * 1000 + w)
+    x = rng.uniform(0, 1, (n, 3, h, w)).astype(np.float32)
+    wt = (rng.standard_normal((cout, 3, 3, 3)) / np.sqrt(27)).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32) * 0.1
+    ref = conv_ref(x.transpose(0, 2, 3, 1), wt, 2, 1, sc, sh, act)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    out = torch.empty(n * ho * wo * cout, device=dev)
+    wk = T(wt.transpose(0, 2, 3, 1).reshape(cout, -1), dev)
+    assert ops.stem_conv_nchw(T(x, dev), wk, T(sc, dev), T(sh, dev), view(out, cout), cout, act=act) == (ho, wo)
+    got = out.cpu().numpy().reshape(-1, cout)
+    # sequential fp32 fmaf chain over 27 taps vs BLAS fp32: reassociation only
+    np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
+
+
 @pytest.mark.parametrize("d", [256, 384, 1000])
 def test_layernorm(dev, d):
     from spotter_amd import ops
