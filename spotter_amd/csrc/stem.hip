@@ -4,7 +4,8 @@
 // K = 27 leaves an implicit GEMM nothing to tile (the MFMA kernels ran it at 12 TF/s, plus an
 // NCHW→NHWC pass over the 157 MB batch), so this is a direct VALU convolution: one lane per output
 // pixel, the 27 taps in registers, the Cout×27 weights uniform across the wave (scalar-cache loads),
-// fmaf chains in the khwc tap order, BN affine + ReLU, Cout floats stored as float4 (NHWC rows).
+// fmaf chains in the khwc tap order, BN affine + ReLU; the workgroup's NHWC rows go out through LDS
+// as coalesced float4 stores.
 // Work per image at 640²: 320²·Cout·27·2 FLOP = 177 MFLOP; compulsory bytes 3·640²·4 in +
 // 320²·Cout·4 out (18 MB at Cout 32) — the output write bounds it.
 #include "common.h"
@@ -12,52 +13,71 @@
 namespace sp {
 namespace {
 
+constexpr int STEM_BLOCK = 256;
+
+// Each lane computes one pixel's CO outputs; the workgroup's 256 consecutive NHWC rows are one
+// contiguous span of y, so the results are staged in LDS (row stride CO+4 floats: 16-byte aligned,
+// rows spread over the banks) and written back as consecutive float4s across the lanes.
 template <int CO>
-__global__ __launch_bounds__(256) void stem_conv_nchw_kernel(
+__global__ __launch_bounds__(STEM_BLOCK) void stem_conv_nchw_kernel(
     const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ scale,
     const float* __restrict__ shift, float* __restrict__ y, int n, int h, int w, int ho, int wo,
     int relu) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int LD = CO + 4;
+  __shared__ float4 tile4[STEM_BLOCK * LD / 4];
+  float* tile = reinterpret_cast<float*>(tile4);
+  const int64_t p0 = (int64_t)blockIdx.x * STEM_BLOCK;
   const int64_t total = (int64_t)n * ho * wo;
-  if (p >= total) return;
-  const int ox = (int)(p % wo);
-  const int64_t q = p / wo;
-  const int oy = (int)(q % ho);
-  const int b = (int)(q / ho);
-  const int64_t hw = (int64_t)h * w;
-  const float* xb = x + (int64_t)b * 3 * hw;
+  const int rows = (int)min<int64_t>(STEM_BLOCK, total - p0);
+  const int t = threadIdx.x;
+  if (t < rows) {
+    const int64_t p = p0 + t;
+    const int ox = (int)(p % wo);
+    const int64_t q = p / wo;
+    const int oy = (int)(q % ho);
+    const int b = (int)(q / ho);
+    const int64_t hw = (int64_t)h * w;
+    const float* xb = x + (int64_t)b * 3 * hw;
 
-  float in[27];
+    float in[27];
 #pragma unroll
-  for (int kh = 0; kh < 3; ++kh) {
-    const int iy = 2 * oy - 1 + kh;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int iy = 2 * oy - 1 + kh;
 #pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int ix = 2 * ox - 1 + kw;
-      const bool ok = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
-      const int64_t off = ok ? (int64_t)iy * w + ix : 0;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ix = 2 * ox - 1 + kw;
+        const bool ok = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+        const int64_t off = ok ? (int64_t)iy * w + ix : 0;
 #pragma unroll
-      for (int ci = 0; ci < 3; ++ci) {
-        const float v = xb[ci * hw + off];
-        in[(kh * 3 + kw) * 3 + ci] = ok ? v : 0.f;
+        for (int ci = 0; ci < 3; ++ci) {
+          const float v = xb[ci * hw + off];
+          in[(kh * 3 + kw) * 3 + ci] = ok ? v : 0.f;
+        }
       }
     }
-  }
 
-  float* yo = y + p * CO;
 #pragma unroll
-  for (int c0 = 0; c0 < CO; c0 += 4) {
-    float a[4];
+    for (int c0 = 0; c0 < CO; c0 += 4) {
+      float a[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float* wr = wt + (c0 + j) * 27;
-      float s = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const float* wr = wt + (c0 + j) * 27;
+        float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 27; ++k) s = fmaf(in[k], wr[k], s);
-      s = fmaf(s, scale[c0 + j], shift[c0 + j]);
-      a[j] = relu ? fmaxf(s, 0.f) : s;
+        for (int k = 0; k < 27; ++k) s = fmaf(in[k], wr[k], s);
+        s = fmaf(s, scale[c0 + j], shift[c0 + j]);
+        a[j] = relu ? fmaxf(s, 0.f) : s;
+      }
+      *reinterpret_cast<float4*>(tile + t * LD + c0) = make_float4(a[0], a[1], a[2], a[3]);
     }
-    *reinterpret_cast<float4*>(yo + c0) = make_float4(a[0], a[1], a[2], a[3]);
+  }
+  __syncthreads();
+  constexpr int C4 = CO / 4;
+  float4* yo = reinterpret_cast<float4*>(y + p0 * CO);
+  const int n4 = rows * C4;
+  for (int i = t; i < n4; i += STEM_BLOCK) {
+    const int r = i / C4, c = i - r * C4;
+    yo[i] = *reinterpret_cast<const float4*>(tile + r * LD + 4 * c);
   }
 }
 
@@ -73,12 +93,12 @@ extern "C" int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const flo
                "sp_stem_conv3x3s2_nchw: bad args (cout must be 32 or 64, act none/relu)");
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const int64_t total = (int64_t)n * ho * wo;
-  const unsigned grid = (unsigned)((total + 255) / 256);
+  const unsigned grid = (unsigned)((total + STEM_BLOCK - 1) / STEM_BLOCK);
   if (cout == 32)
-    hipLaunchKernelGGL(stem_conv_nchw_kernel<32>, dim3(grid), dim3(256), 0, as_stream(stream), x, wt, scale,
+    hipLaunchKernelGGL(stem_conv_nchw_kernel<32>, dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt, scale,
                        shift, y, n, h, w, ho, wo, act);
   else
-    hipLaunchKernelGGL(stem_conv_nchw_kernel<64>, dim3(grid), dim3(256), 0, as_stream(stream), x, wt, scale,
+    hipLaunchKernelGGL(stem_conv_nchw_kernel<64>, dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt, scale,
                        shift, y, n, h, w, ho, wo, act);
   return check_launch("sp_stem_conv3x3s2_nchw");
 }
