@@ -131,10 +131,11 @@ int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* 
  * act 0 (none) or 1 (relu). (ABI v6) */
 int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, const float* shift, float* y,
                            int n, int h, int w, int cout, int act, void* stream);
-/* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). */
-int sp_maxpool3x3s2(const float* x, float* y, int n, int h, int w, int c, void* stream);
-/* nn.AvgPool2d(2, 2, 0, ceil_mode=True) on NHWC (RN:150, RN:202). */
-int sp_avgpool2x2_ceil(const float* x, float* y, int n, int h, int w, int c, void* stream);
+/* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
+ * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
+int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);
+/* nn.AvgPool2d(2, 2, 0, ceil_mode=True) on NHWC (RN:150, RN:202); y rows ldy floats apart as above. */
+int sp_avgpool2x2_ceil(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);
 /* F.interpolate(scale_factor=2, mode="nearest") into a channel slice (M2:1192). */
 int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, int n, int h,
                           int w, int c, void* stream);

@@ -66,8 +66,8 @@ _SIGS = {
     "sp_conv2d": (i32, [C.POINTER(SpConvDesc), vp]),
     "sp_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "sp_stem_conv3x3s2_nchw": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
-    "sp_maxpool3x3s2": (i32, [vp, vp, i32, i32, i32, i32, vp]),
-    "sp_avgpool2x2_ceil": (i32, [vp, vp, i32, i32, i32, i32, vp]),
+    "sp_maxpool3x3s2": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
+    "sp_avgpool2x2_ceil": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
     "sp_upsample2x_nearest": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_layernorm": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),
     "sp_attention": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),

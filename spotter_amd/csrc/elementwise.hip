@@ -19,7 +19,7 @@ inline unsigned grid_for(int64_t work, int block = 256) {
 
 // c4 = channels / 4
 __global__ void maxpool3s2_kernel(const float4* __restrict__ x, float4* __restrict__ y, int n, int h,
-                                  int w, int c4, int ho, int wo) {
+                                  int w, int c4, int ho, int wo, int64_t ldy4) {
   const int64_t total = (int64_t)n * ho * wo * c4;
   for (int64_t i = gtid(); i < total; i += grid_stride()) {
     int cc = (int)(i % c4);
@@ -39,12 +39,12 @@ __global__ void maxpool3s2_kernel(const float4* __restrict__ x, float4* __restri
         m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
       }
     }
-    y[i] = m;
+    y[p * ldy4 + cc] = m;
   }
 }
 
 __global__ void avgpool2_kernel(const float4* __restrict__ x, float4* __restrict__ y, int n, int h,
-                                int w, int c4, int ho, int wo) {
+                                int w, int c4, int ho, int wo, int64_t ldy4) {
   const int64_t total = (int64_t)n * ho * wo * c4;
   for (int64_t i = gtid(); i < total; i += grid_stride()) {
     int cc = (int)(i % c4);
@@ -67,7 +67,7 @@ __global__ void avgpool2_kernel(const float4* __restrict__ x, float4* __restrict
       }
     }
     const float inv = (float)cnt;
-    y[i] = make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
+    y[p * ldy4 + cc] = make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
   }
 }
 
@@ -187,21 +187,26 @@ extern "C" int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, in
   return check_launch("sp_nchw_to_nhwc");
 }
 
-extern "C" int sp_maxpool3x3s2(const float* x, float* y, int n, int h, int w, int c, void* stream) {
-  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "sp_maxpool3x3s2: bad args");
+extern "C" int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && ldy >= c && ldy % 4 == 0 &&
+                   ((uintptr_t)y & 15) == 0,
+               "sp_maxpool3x3s2: bad args");
   int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   int64_t work = (int64_t)n * ho * wo * (c / 4);
   hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
-                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo);
+                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4);
   return check_launch("sp_maxpool3x3s2");
 }
 
-extern "C" int sp_avgpool2x2_ceil(const float* x, float* y, int n, int h, int w, int c, void* stream) {
-  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "sp_avgpool2x2_ceil: bad args");
+extern "C" int sp_avgpool2x2_ceil(const float* x, float* y, int64_t ldy, int n, int h, int w, int c,
+                                  void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0 && ldy >= c && ldy % 4 == 0 &&
+                   ((uintptr_t)y & 15) == 0,
+               "sp_avgpool2x2_ceil: bad args");
   int ho = (h + 1) / 2, wo = (w + 1) / 2;
   int64_t work = (int64_t)n * ho * wo * (c / 4);
   hipLaunchKernelGGL(avgpool2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
-                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo);
+                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4);
   return check_launch("sp_avgpool2x2_ceil");
 }
 

@@ -135,13 +135,14 @@ class Engine:
     """Owns the packed device weights and the per-shape workspaces of one GPU."""
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
-                 fold_repvgg: bool = True, precision: str = "fp32"):
+                 fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True):
         from ._lib import lib
 
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
+        self.fuse_shortcut = fuse_shortcut  # bottleneck tail + projection shortcut as one GEMM (_fused_tail)
         self.precision = precision
         self._conv_mode, self._lin_mode = PRECISIONS[precision]
         self.dev = torch.device(device)
@@ -223,6 +224,9 @@ class Engine:
             nl = 3 if lt == "bottleneck" else 2
             blk["layers"] = [self._conv(p, f"{pre}.layer.{j}.convolution.weight", f"{pre}.layer.{j}.normalization", True)
                              for j in range(nl)]
+            if self.fuse_shortcut and lt == "bottleneck" and (sc == "avgconv" or (sc == "conv" and st == 1)):
+                sk = pre + (".shortcut.1" if sc == "avgconv" else ".shortcut")
+                blk["fused"] = self._fused_tail(p, f"{pre}.layer.2", sk, cin)
             self.blocks.append(blk)
         self.in_proj = [self._conv(p, f"model.encoder_input_proj.{l}.0.weight", f"model.encoder_input_proj.{l}.1", False)
                         for l in range(len(cfg.encoder_in_channels))]
@@ -273,6 +277,21 @@ class Engine:
                 "bbox": [self._lin(p, f"model.decoder.bbox_embed.{j}.layers.{i}", **pq) for i in range(3)],
             })
         self.cls_last = self._lin(p, f"model.decoder.class_embed.{L - 1}")
+
+    def _fused_tail(self, p, conv3, short, cin):
+        """Bottleneck tail + projection shortcut as one 1×1 GEMM over K = red + cin (RN:199-207, 225-231):
+        relu(BN3(W3·t2) + BNsc(Wsc·x)) = relu([s3·W3 | ssc·Wsc]·[t2 | x] + (b3 + bsc)). The producers write
+        t2 and the (pooled) block input side by side in one NHWC buffer, so the shortcut's Cout-wide
+        output never goes through HBM. BN scales fold into the weights in f64, rounded once to f32."""
+        w3 = conv_khwc(p[conv3 + ".convolution.weight"]).astype(np.float64)
+        wsc = conv_khwc(p[short + ".convolution.weight"]).astype(np.float64)
+        s3, b3 = frozen_bn_affine(p, conv3 + ".normalization")
+        ss, bs = frozen_bn_affine(p, short + ".normalization")
+        wf = np.concatenate([w3 * s3.astype(np.float64)[:, None], wsc * ss.astype(np.float64)[:, None]], 1)
+        co, kc = wf.shape
+        assert kc == w3.shape[1] + cin
+        shift = b3.astype(np.float64) + bs.astype(np.float64)
+        return self._mk_conv(wf.astype(np.float32), kc, co, 1, np.ones(co, np.float32), shift.astype(np.float32))
 
     def _csp(self, p, pre):
         c1 = self._conv(p, pre + ".conv1.conv.weight", pre + ".conv1.norm", False)
@@ -358,16 +377,43 @@ class Engine:
         self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act="relu")
         self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act="relu")
         h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
-        cur = self._buf("pool", B, h, w, e)
-        ops.maxpool3x3s2(s2, cur, B, h1, w1, e)
+        b0 = self.blocks[0]
+        if "fused" in b0 and b0["sc"] == "conv":
+            # the first block's fused tail reads the pooled stem next to its conv2 output: pool into that slice
+            kc = b0["layers"][0].cout + e
+            curv = V(self._buf(f"s{b0['s']}_cat", B, h, w, kc), kc - e, kc)
+        else:
+            curv = view(self._buf("pool", B, h, w, e), e)
+        ops.maxpool3x3s2(s2, curv, B, h1, w1, e)
         c = e
         feats = []
         nstage = len(self.cfg.depths)
         for blk in self.blocks:
             s, i, st, cout = blk["s"], blk["i"], blk["stride"], blk["cout"]
+            cur = curv.t
             if i == 0 and s > 0:
+                assert curv.off == 0 and curv.ld == c
                 feats.append((cur, h, w, c))
             ho, wo = (h - 1) // st + 1, (w - 1) // st + 1
+            L = blk["layers"]
+            if "fused" in blk:
+                red = L[0].cout
+                kc = red + c
+                if blk["sc"] == "avgconv":
+                    assert curv.off == 0 and curv.ld == c
+                    cat = self._buf(f"s{s}_cat", B, ho, wo, kc)
+                    ops.avgpool2x2_ceil(cur, V(cat, red, kc), B, h, w, c)
+                else:  # stride-1 projection: the block input already sits in the slice (see above)
+                    assert curv.off == red and curv.ld == kc and st == 1
+                    cat = cur
+                t1 = self._buf(f"s{s}_t1", B, h, w, red)
+                out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
+                self._cv(curv, B, h, w, L[0], 1, view(t1, red), act="relu")
+                self._cv(view(t1, red), B, h, w, L[1], st, V(cat, 0, kc), act="relu")
+                self._cv(V(cat, 0, kc), B, ho, wo, blk["fused"], 1, view(out, cout), act="relu")
+                curv, h, w, c = view(out, cout), ho, wo, cout
+                yield
+                continue
             # shortcut (RN:199-207)
             if blk["sc"] == "identity":
                 res = view(cur, c)
@@ -381,7 +427,6 @@ class Engine:
                 self._cv(view(src, c), B, sh_, sw_, blk["short"], 1 if blk["sc"] == "avgconv" else st, view(sbuf, cout))
                 res = view(sbuf, cout)
             out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
-            L = blk["layers"]
             if blk["type"] == "bottleneck":
                 red = L[0].cout
                 t1 = self._buf(f"s{s}_t1", B, h, w, red)
@@ -393,9 +438,9 @@ class Engine:
                 t1 = self._buf(f"s{s}_t1", B, ho, wo, cout)
                 self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act="relu")
                 self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act="relu", res1=res)
-            cur, h, w, c = out, ho, wo, cout
+            curv, h, w, c = view(out, cout), ho, wo, cout
             yield
-        feats.append((cur, h, w, c))
+        feats.append((curv.t, h, w, c))
         return feats[-3:] if nstage >= 3 else feats
 
     def _csp_fwd(self, cs, x: V, B, h, w, out: V, tag):

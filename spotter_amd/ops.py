@@ -186,18 +186,31 @@ def stem_conv_nchw(x: torch.Tensor, wt: torch.Tensor, scale: torch.Tensor, shift
     return ho, wo
 
 
-def maxpool3x3s2(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
+def _pool_out(y, m: int, c: int, what: str):
+    """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
+    if isinstance(y, V):
+        if y.ld % 4 or y.off % 4:
+            raise ValueError(f"{what}: output view must be float4-aligned")
+        return y.need(m, c, what), y.ld
+    if y.numel() < m * c:
+        raise ValueError(f"{what}: output too small")
+    return y.data_ptr(), c
+
+
+def maxpool3x3s2(x: torch.Tensor, y, n, h, w, c):
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
-    assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
-    _launch("elementwise", "sp_maxpool3x3s2", (x.data_ptr(), y.data_ptr(), n, h, w, c, stream()), 0,
+    assert x.numel() >= n * h * w * c
+    yp, ldy = _pool_out(y, n * ho * wo, c, "maxpool.y")
+    _launch("elementwise", "sp_maxpool3x3s2", (x.data_ptr(), yp, ldy, n, h, w, c, stream()), 0,
             4 * n * c * (h * w + ho * wo))
     return ho, wo
 
 
-def avgpool2x2_ceil(x: torch.Tensor, y: torch.Tensor, n, h, w, c):
+def avgpool2x2_ceil(x: torch.Tensor, y, n, h, w, c):
     ho, wo = (h + 1) // 2, (w + 1) // 2
-    assert x.numel() >= n * h * w * c and y.numel() >= n * ho * wo * c
-    _launch("elementwise", "sp_avgpool2x2_ceil", (x.data_ptr(), y.data_ptr(), n, h, w, c, stream()), 0,
+    assert x.numel() >= n * h * w * c
+    yp, ldy = _pool_out(y, n * ho * wo, c, "avgpool.y")
+    _launch("elementwise", "sp_avgpool2x2_ceil", (x.data_ptr(), yp, ldy, n, h, w, c, stream()), 0,
             4 * n * c * (h * w + ho * wo))
     return ho, wo
 

@@ -275,6 +275,25 @@ def test_nchw_to_nhwc(dev):
     np.testing.assert_array_equal(y.cpu().numpy().reshape(2, 5, 7, 3), x.transpose(0, 2, 3, 1))
 
 
+def test_pools_into_channel_slice(dev):
+    """Pools writing a channel slice of a wider buffer (ldy > c): the fused bottleneck shortcut's layout."""
+    from oracle.rtdetr_np import avgpool2_ceil, maxpool3s2
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(5)
+    n, h, w, c, red = 2, 9, 7, 8, 12
+    x = rng.standard_normal((n, h, w, c)).astype(np.float32)
+    xt = T(x.reshape(-1), dev)
+    for fn, ref, (ho, wo) in ((ops.maxpool3x3s2, maxpool3s2, ((h - 1) // 2 + 1, (w - 1) // 2 + 1)),
+                              (ops.avgpool2x2_ceil, avgpool2_ceil, ((h + 1) // 2, (w + 1) // 2))):
+        y = torch.full((n * ho * wo * (red + c),), 7.0, device=dev)
+        fn(xt, V(y, red, red + c), n, h, w, c)
+        got = y.cpu().numpy().reshape(n, ho, wo, red + c)
+        np.testing.assert_allclose(got[..., red:], ref(x), rtol=1e-6, atol=1e-6)
+        assert np.all(got[..., :red] == 7.0)
+
+
 @pytest.mark.parametrize("case", [(1, 17, 15, 32, "relu"), (2, 640, 640, 32, "relu"), (3, 33, 8, 64, None),
                                   (1, 1, 1, 32, "relu")])
 def test_stem_conv_nchw(dev, case):

@@ -39,11 +39,16 @@ SHAPES = [
     (32, 20, 20, 384, 384, 3, 1, None, False, 3),       # 17 CCFM 3x3 @20²
     (32, 20, 20, 512, 2048, 1, 1, "relu", True, 3),     # 18 stage4 expand
     (32, 80, 80, 512, 128, 1, 1, "relu", False, 3),     # 19 stage1 reduce
+    # fused bottleneck tail + projection shortcut (engine._fused_tail): K = red + cin
+    (32, 160, 160, 128, 256, 1, 1, "relu", False, 1),   # 20 stage0 block0 fused tail
+    (32, 80, 80, 384, 512, 1, 1, "relu", False, 1),     # 21 stage1 block0 fused tail
+    (32, 40, 40, 768, 1024, 1, 1, "relu", False, 1),    # 22 stage2 block0 fused tail
+    (32, 20, 20, 1536, 2048, 1, 1, "relu", False, 1),   # 23 stage3 block0 fused tail
     # bs1 /detect latency path (run with --ws: the engine hands every conv a split-K workspace)
-    (1, 80, 80, 384, 384, 3, 1, None, False, 3),        # 20 CCFM 3x3 @80² bs1
-    (1, 40, 40, 256, 256, 3, 1, "relu", False, 22),     # 21 stage3 3x3 bs1
-    (1, 40, 40, 1024, 256, 1, 1, "relu", False, 22),    # 22 stage3 reduce bs1
-    (1, 40, 40, 256, 1024, 1, 1, "relu", True, 23),     # 23 stage3 expand bs1
+    (1, 80, 80, 384, 384, 3, 1, None, False, 3),        # 24 CCFM 3x3 @80² bs1
+    (1, 40, 40, 256, 256, 3, 1, "relu", False, 22),     # 25 stage3 3x3 bs1
+    (1, 40, 40, 1024, 256, 1, 1, "relu", False, 22),    # 26 stage3 reduce bs1
+    (1, 40, 40, 256, 1024, 1, 1, "relu", True, 23),     # 27 stage3 expand bs1
 ]
 
 
