@@ -159,3 +159,24 @@ def test_bf16_variant_close_to_fp32_goldens():
     d = delta("r18vd")
     assert d["recall_vs_fp32"] >= 0.8, d
     assert d["p95_dscore"] <= 0.05, d
+
+
+def test_fused_bottleneck_tail_matches_unfused():
+    """The fused conv3 + projection-shortcut GEMM (Engine._fused_tail: BN scales folded into the weights,
+    K = red + cin) against the separate shortcut GEMM + residual epilogue it replaces, on R101vd (the
+    first block of each of the 4 stages is fused). fp32 reassociation only: compare at the parity bar."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+    from spotter_amd.synthetic import synthetic_image
+
+    cfg = PRESETS["r101vd"]
+    w = SpotterForObjectDetection(cfg)._host_weights()
+    x = SpotterImageProcessor()(images=synthetic_image(11))["pixel_values"].cuda()
+    res = []
+    for fuse in (True, False):
+        eng = Engine(cfg, w, "cuda", fuse_shortcut=fuse)
+        assert sum("fused" in b for b in eng.blocks) == (4 if fuse else 0)
+        lg, bx = eng.forward(x)
+        res.append((torch.sigmoid(lg[0]).cpu().numpy().max(-1), bx[0].cpu().numpy()))
+    np.testing.assert_allclose(np.sort(res[0][0]), np.sort(res[1][0]), rtol=0, atol=SCORE_TOL)
