@@ -4,7 +4,7 @@ Per MI355X_MICROARCH.md (HBM section): rocprofv3's FETCH_SIZE / WRITE_SIZE are i
 FETCH_SIZE counts half the bytes of wide (16 B/lane) coalesced reads, so it is doubled; WRITE_SIZE
 is exact for 16 B/lane stores (the conv epilogue's float4 stores). HBM bytes = 2·FETCH + WRITE.
 The conv class includes the split-K reduce kernel of the same sp_conv2d call; per-launch figures
-divide by the number of conv_gemm dispatches (one per sp_conv2d call).
+divide by the number of conv dispatches (one per sp_conv2d call, plus the direct stem conv).
 
     python tools/pmc_reduce.py <outdir> [bench args]   # writes/updates profiles/pmc_traffic.json
 """
@@ -16,7 +16,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce")), ("msda", ("msda",)), ("attention", ("attn_",)),
+CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce", "stem_conv")), ("msda", ("msda",)), ("attention", ("attn_",)),
            ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)), ("layernorm", ("layernorm",))]
 LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_", "preprocess": None, "topk": "topk",
            "layernorm": "layernorm"}

@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
+CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "stem_conv")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
            ("attention", ("attn_",)), ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)),
            ("layernorm", ("layernorm",)), ("postprocess_decode", ("decode_kernel",))]
 
