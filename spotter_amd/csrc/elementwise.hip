@@ -123,6 +123,52 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
+// float4 variant (d, ldx, ldy multiples of 4, 16-byte aligned rows): one wave per row, up to 4 float4
+// per lane (d <= 1024). Same two-pass mean / variance as above, 4x fewer load / store instructions.
+__global__ __launch_bounds__(256) void layernorm4_kernel(const float* __restrict__ x, int64_t ldx,
+                                                          const float* __restrict__ g,
+                                                          const float* __restrict__ b,
+                                                          float* __restrict__ y, int64_t ldy,
+                                                          int rows, int d, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int d4 = d >> 2;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+  float4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < d4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < d4) {
+      const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+      q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+  }
+  const float var = wave_sum(q) / (float)d;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  float4* yr = reinterpret_cast<float4*>(y + row * ldy);
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(b);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < d4) {
+      const float4 gg = g4[c], bb = b4[c];
+      yr[c] = make_float4((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y,
+                          (v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+    }
+  }
+}
+
 __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src, int src_rows,
                                    const int32_t* __restrict__ idx, int k, int batch, int d,
                                    float* __restrict__ dst, int64_t ld_dst) {
@@ -222,8 +268,10 @@ extern "C" int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int6
 extern "C" int sp_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float* y,
                             int64_t ldy, int rows, int d, float eps, void* stream) {
   SP_ARG_CHECK(x && gamma && beta && y && rows > 0 && d > 0 && d <= 1024, "sp_layernorm: bad args");
-  hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, ldx,
-                     gamma, beta, y, ldy, rows, d, eps);
+  const bool vec = d % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 &&
+                  (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0;
+  hipLaunchKernelGGL(vec ? layernorm4_kernel : layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0,
+                     as_stream(stream), x, ldx, gamma, beta, y, ldy, rows, d, eps);
   return check_launch("sp_layernorm");
 }
 

@@ -319,7 +319,7 @@ def test_stem_conv_nchw(dev, case):
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("d", [256, 384, 1000])
+@pytest.mark.parametrize("d", [256, 258, 384, 1000])  # 258: scalar path, others: float4 path
 def test_layernorm(dev, d):
     from spotter_amd import ops
     from spotter_amd.ops import view
