@@ -1,5 +1,5 @@
 set -euo pipefail
-OUT=gpurun_out/r1_final
+OUT=gpurun_out/${1:-r1_final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
