@@ -44,31 +44,32 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const float4* __restric
   }
 }
 
-__global__ void avgpool2_kernel(const float4* __restrict__ x, float4* __restrict__ y, int n, int h,
-                                int w, int c4, int ho, int wo, int64_t ldy4) {
-  const int64_t total = (int64_t)n * ho * wo * c4;
-  for (int64_t i = gtid(); i < total; i += grid_stride()) {
-    int cc = (int)(i % c4);
-    int64_t p = i / c4;
-    int ox = (int)(p % wo);
-    int64_t q = p / wo;
-    int oy = (int)(q % ho);
-    int b = (int)(q / ho);
+// Same 2-D grid as maxpool3s2_kernel: output rows over blockIdx.y, wo·c4 float4s over x.
+__global__ __launch_bounds__(256) void avgpool2_kernel(const float4* __restrict__ x, float4* __restrict__ y,
+                                                       int n, int h, int w, int c4, int ho, int wo, int64_t ldy4) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= wo * c4) return;
+  const int ox = j / c4, cc = j - ox * c4;
+  for (int row = blockIdx.y; row < n * ho; row += gridDim.y) {  // row = b * ho + oy
+    const int oy = row % ho, b = row / ho;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     int cnt = 0;
+#pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
-      int iy = oy * 2 + dy;
+      const int iy = oy * 2 + dy;
       if (iy >= h) continue;
+      const float4* xr = x + ((int64_t)b * h + iy) * w * c4 + cc;
+#pragma unroll
       for (int dx = 0; dx < 2; ++dx) {
-        int ix = ox * 2 + dx;
+        const int ix = ox * 2 + dx;
         if (ix >= w) continue;
-        float4 v = x[(((int64_t)b * h + iy) * w + ix) * c4 + cc];
+        const float4 v = xr[ix * c4];
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         ++cnt;
       }
     }
     const float inv = (float)cnt;
-    y[p * ldy4 + cc] = make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
+    y[((int64_t)row * wo + ox) * ldy4 + cc] = make_float4(s.x / inv, s.y / inv, s.z / inv, s.w / inv);
   }
 }
 
@@ -252,8 +253,9 @@ extern "C" int sp_avgpool2x2_ceil(const float* x, float* y, int64_t ldy, int n, 
                    ((uintptr_t)y & 15) == 0,
                "sp_avgpool2x2_ceil: bad args");
   int ho = (h + 1) / 2, wo = (w + 1) / 2;
-  int64_t work = (int64_t)n * ho * wo * (c / 4);
-  hipLaunchKernelGGL(avgpool2_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+  SP_ARG_CHECK((int64_t)n * ho < (1 << 30) && (int64_t)wo * (c / 4) < (1 << 30), "sp_avgpool2x2_ceil: size out of range");
+  const int gy = n * ho < 65535 ? n * ho : 65535;
+  hipLaunchKernelGGL(avgpool2_kernel, dim3((wo * (c / 4) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
                      (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4);
   return check_launch("sp_avgpool2x2_ceil");
 }
