@@ -8,9 +8,18 @@ gloo process group only provides the barrier and the max-over-ranks time.
 
     python bench.py [--gpus N --steps K --warmup W --batch 32 --preset r101vd --size 640]
 
+--gpus N > 1 without a torch.distributed launcher: the parent process spawns N
+replica processes BEFORE any GPU call, each pinned to one device with
+HIP_VISIBLE_DEVICES (one Serve replica per GPU); under
+`torch.distributed.run` (WORLD_SIZE set) each rank is already a replica and uses
+cuda:LOCAL_RANK. Either way the ranks meet only in a gloo barrier and the max
+of their elapsed times; value = all ranks' images / that max.
+
 Prints ONE JSON line (rank 0) with the contract fields plus `roofline` (the
-dominant kernel: the fp32 MFMA implicit-GEMM conv, HIP-event timed inside the
-timed region) and `cpu_baseline` (the reference HF path on the host CPU).
+dominant kernel: the fp32-accurate 3-way-split implicit-GEMM conv, HIP-event
+timed inside the timed region, priced against ITS pipe ceiling: 2500/6 TFLOP/s
+fp32-equivalent on the bf16 MFMA) and `cpu_baseline` (the reference HF path on
+the host CPU, bs32 and bs1 legs, median of 3 timed runs each).
 """
 from __future__ import annotations
 
@@ -25,6 +34,8 @@ sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 / 16x16x4
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 (v_mfma_f32_32x32x16_bf16), not the 2:1-sparse figure
+X3_MFMA_PER_BLOCK = 6  # the fp32-accurate split issues 6 bf16 MFMAs per fp32 32x32x16 product block
+X3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / X3_MFMA_PER_BLOCK  # fp32-equivalent ceiling of that kernel
 HBM_PEAK_GBS = 8000.0
 BASELINE_METRIC = "images/sec RT-DETRv2-R101 640\u00b2 bs32 at 1/2/4/8 MI355X; p50 /detect latency"
 
@@ -37,7 +48,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=4.0,
+                    help="minimum duration of each timed bs1 CPU run (3 runs, median)")
+    ap.add_argument("--cpu-baseline-batch", type=int, default=32,
+                    help="batch of the CPU comparison leg (BASELINE.md §3: bs32; 0 = bs1 leg only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--latency-iters", type=int, default=100,
@@ -50,6 +64,7 @@ def parse():
     ap.add_argument("--microbatches", type=int, default=1,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
+    ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU launcher test
     return ap.parse_args()
 
 
@@ -118,8 +133,9 @@ class KernelEventRecorder:
         for k, e0, e1, f, nb, shp in self.recs:
             if k != "conv" or not shp or len(shp) < 6:
                 continue
-            c = out.setdefault(shp[5], {"flops": 0, "ms": 0.0, "n": 0})
+            c = out.setdefault(shp[5], {"flops": 0, "bytes": 0, "ms": 0.0, "n": 0})
             c["flops"] += f
+            c["bytes"] += nb
             c["ms"] += e0.elapsed_time(e1)
             c["n"] += 1
         return out
@@ -140,26 +156,28 @@ class KernelEventRecorder:
         return out
 
 
-def load_traffic(args, avg_alg_bytes):
-    """HBM bytes per conv launch from the committed PMC passes (tools/pmc_bench.py), if they were
-    collected on this exact configuration; null otherwise."""
+def load_traffic(args, avg_alg_bytes, key="conv"):
+    """HBM bytes per launch of kernel class `key` from the committed PMC passes
+    (tools/pmc_bench.sh), if they were collected on this exact configuration; null otherwise."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         t = json.load(f)
-    key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.microbatches}"
-    e = t.get(key)
+    cfg_key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.microbatches}"
+    e = (t.get(cfg_key) or {}).get("classes", {}).get(key)
     if not e:
         return None, None
-    return e["conv_hbm_bytes_per_launch"], {"source": f"profiles/pmc_traffic.json[{key}]",
-                                            "ratio_to_algorithmic": round(e["conv_hbm_bytes_per_launch"]
-                                                                          / avg_alg_bytes, 3)}
+    b = e["hbm_bytes_per_launch"]
+    return b, {"source": f"profiles/pmc_traffic.json[{cfg_key}].classes.{key}",
+               "ratio_to_algorithmic": round(b / avg_alg_bytes, 3)}
 
 
-def cpu_baseline(cfg, weights, seconds):
+def cpu_baseline(cfg, weights, seconds, batch):
     """Reference CPU path (HF RTDetrImageProcessorPil → RTDetrV2ForObjectDetection fp32 →
-    post_process_object_detection), bs=1 as /detect runs it (serve.py:96-109), on the host cores."""
+    post_process_object_detection) on the host cores, per BASELINE.md §3: a bs1 leg as /detect
+    runs it (serve.py:96-109) and a bs`batch` leg (the ≥50× comparison), each 1 warmup + 3 timed
+    runs, median images/sec. `value` is the bs`batch` leg (the bs1 leg when batch <= 1)."""
     import numpy as np
     import torch
     from PIL import Image
@@ -172,58 +190,169 @@ def cpu_baseline(cfg, weights, seconds):
     torch.set_num_threads(ncores)
     model = build_hf_model(cfg, weights)
     proc = build_hf_processor()
-    imgs = [Image.fromarray(synthetic_image(500 + i, cfg.image_size, cfg.image_size)) for i in range(4)]
+    S = cfg.image_size
+    imgs = [Image.fromarray(synthetic_image(500 + i, S, S)) for i in range(max(4, batch))]
 
-    def one(im):
-        inp = proc(images=im, return_tensors="pt")
+    def run(ims):
+        inp = proc(images=ims, return_tensors="pt")
         with torch.no_grad():
             out = model(**inp)
-        proc.post_process_object_detection(out, target_sizes=torch.tensor([[im.size[1], im.size[0]]]),
+        proc.post_process_object_detection(out, target_sizes=torch.tensor([[im.size[1], im.size[0]] for im in ims]),
                                            threshold=0.5)
 
-    one(imgs[0])  # warmup
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        one(imgs[n % len(imgs)])
-        n += 1
-        if time.perf_counter() - t0 >= seconds and n >= 3:
-            break
-    dt = time.perf_counter() - t0
+    def leg(bs, min_s):
+        run(imgs[:bs])  # warmup
+        rates, walls = [], []
+        for _ in range(3):
+            n, t0 = 0, time.perf_counter()
+            while True:
+                run(imgs[(n // bs * bs) % len(imgs):][:bs] if bs > 1 else [imgs[n % len(imgs)]])
+                n += bs
+                if time.perf_counter() - t0 >= min_s:
+                    break
+            walls.append(time.perf_counter() - t0)
+            rates.append(n / walls[-1])
+        return {"value": float(np.median(rates)), "runs": [round(r, 3) for r in rates],
+                "seconds": round(sum(walls), 1), "batch": bs}
+
+    legs = {"bs1": leg(1, seconds)}
+    if batch > 1:
+        legs[f"bs{batch}"] = leg(batch, 0.0)  # one bs`batch` forward per timed run
+    main_leg = legs[f"bs{batch}"] if batch > 1 else legs["bs1"]
     cpu_model = None
     try:
         with open("/proc/cpuinfo") as f:
             cpu_model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
     except OSError:
         pass
-    return {"value": n / dt, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "reference",
-            "cpu_model": cpu_model,
-            "sample": f"{n} images bs=1 {cfg.image_size}x{cfg.image_size} through HF transformers "
-                      f"RTDetrImageProcessorPil+RTDetrV2ForObjectDetection(fp32, synthetic {cfg.name} weights)"
-                      f"+post_process_object_detection on {torch.get_num_threads()} host threads, {dt:.1f}s"}
+    nt = torch.get_num_threads()
+    return {"value": round(main_leg["value"], 3), "unit": "images/sec", "cores": nt, "kind": "reference",
+            "cpu_model": cpu_model, "legs": legs,
+            "sample": f"HF transformers RTDetrImageProcessorPil+RTDetrV2ForObjectDetection(fp32, synthetic "
+                      f"{cfg.name} weights)+post_process_object_detection on {nt} host threads, "
+                      f"{S}x{S} synthetic images; value = bs{main_leg['batch']} leg, median of 3 timed runs "
+                      f"after 1 warmup (bs1 leg: 3 runs of >= {seconds:g} s)"}
 
 
-def main():
-    args = parse()
-    import numpy as np
+def _visible_devices():
+    for var in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            return [d.strip() for d in v.split(",") if d.strip()]
+    return None
+
+
+def launch_replicas(args) -> int:
+    """--gpus N without a distributed launcher: N replica processes, spawned before this process
+    touches any GPU, replica i pinned to device i by HIP_VISIBLE_DEVICES. Rank 0's
+    stdout (the JSON line) passes through; the other ranks' stdout goes to stderr."""
+    import socket
+    import subprocess
+
+    n = args.gpus
+    vis = _visible_devices()
+    if vis is not None and len(vis) < n:
+        print(f"bench.py: --gpus {n} but only {len(vis)} visible devices ({','.join(vis)})", file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for i in range(n):
+        env = dict(os.environ)
+        dev = vis[i] if vis is not None else str(i)
+        env.update(RANK=str(i), WORLD_SIZE=str(n), LOCAL_RANK=str(i), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HIP_VISIBLE_DEVICES=dev,
+                   CUDA_VISIBLE_DEVICES=dev, SPOTTER_REPLICA_DEVICE="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=None if i == 0 else sys.stderr))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+            if rc:
+                break
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+def conv_roofline(rec, cl, args, bf):
+    """The dominant kernel's roofline. fp32 (the parity path): the 3-way-split kernel (x3 mode),
+    priced against its own pipe ceiling, 2500/6 TF fp32-equivalent (six bf16 MFMAs per fp32
+    32x32x16 block); the fp32-MFMA figure stays as a secondary field. Other precisions: the
+    whole conv class against the mode's MFMA peak."""
+    modes = {}
+    per_mfma = {"x3": (X3_MFMA_PER_BLOCK, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
+                "bf16": (1, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
+                "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS),
+                "direct": (1, "v_fma_f32 (VALU stem conv, no MFMA)", FP32_MFMA_PEAK_TFLOPS)}
+    cm = rec.conv_modes()
+    for md, c in cm.items():
+        a = c["flops"] / (c["ms"] * 1e-3) / 1e12
+        mult, instr, pk = per_mfma[md]
+        modes[md] = {"flop_share": round(c["flops"] / max(1, cl["conv"]["flops"]), 4),
+                     "ms_per_step": round(c["ms"] / args.steps, 3), "launches_per_step": c["n"] // args.steps,
+                     "avg_launch_ms": round(c["ms"] / c["n"], 4),
+                     "achieved": round(a, 2), "unit": "TFLOP/s", "frac_of_mode_ceiling": round(a * mult / pk, 4),
+                     "mfma_issue": {"instr": instr, "mfma_per_fp32_block": mult,
+                                    "achieved": round(mult * a, 1), "peak": pk, "frac": round(mult * a / pk, 4)}}
+    c = cl["conv"]
+    if args.precision == "fp32" and "x3" in cm:
+        x = cm["x3"]
+        ach = x["flops"] / (x["ms"] * 1e-3) / 1e12
+        alg_bytes = x["bytes"] / x["n"]
+        traffic, tnote = load_traffic(args, alg_bytes, key="conv_x3")
+        roof = {"bound": "mfma", "kernel": "conv x3 kernels (fp32 operands split hi/mid/lo bf16, 6 "
+                                           "v_mfma_f32_32x32x16_bf16 per fp32 32x32x16 block, implicit GEMM)",
+                "achieved": round(ach, 2), "peak": round(X3_PEAK_TFLOPS, 2), "unit": "TFLOP/s",
+                "frac": round(ach / X3_PEAK_TFLOPS, 4), "traffic": traffic,
+                "peak_note": "fp32-equivalent ceiling of the split kernel = dense bf16 MFMA 2500 TF / 6",
+                "vs_fp32_mfma_peak": {"peak": FP32_MFMA_PEAK_TFLOPS, "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)},
+                "launches_per_step": x["n"] // args.steps, "avg_launch_ms": round(x["ms"] / x["n"], 4),
+                "gflop_per_launch": round(x["flops"] / x["n"] / 1e9, 3),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "flop_share_of_conv_class": round(x["flops"] / max(1, c["flops"]), 4),
+                "conv_class": {"achieved": round(c["flops"] / (c["busy"] * 1e-3) / 1e12, 2),
+                               "ms_per_step": round(c["busy"] / args.steps, 3),
+                               "launches_per_step": c["n"] // args.steps,
+                               "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2)},
+                "note": "achieved = algorithmic fp32 FLOPs of the x3 launches / the sum of their durations "
+                        "(HIP events on the launch stream); traffic = HBM bytes per x3 launch from PMC "
+                        "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
+    else:
+        conv_peak = BF16_MFMA_PEAK_TFLOPS if bf else FP32_MFMA_PEAK_TFLOPS
+        ach = c["flops"] / (c["busy"] * 1e-3) / 1e12
+        alg_bytes = c["bytes"] / c["n"]
+        traffic, tnote = load_traffic(args, alg_bytes)
+        roof = {"bound": "mfma", "kernel": f"conv class ({args.precision})", "achieved": round(ach, 2),
+                "peak": conv_peak, "unit": "TFLOP/s", "frac": round(ach / conv_peak, 4), "traffic": traffic,
+                "launches_per_step": c["n"] // args.steps, "avg_launch_ms": round(c["ms"] / c["n"], 4),
+                "gflop_per_launch": round(c["flops"] / c["n"] / 1e9, 3),
+                "algorithmic_bytes_per_launch": int(alg_bytes),
+                "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2)}
+    if tnote:
+        roof["traffic_source"] = tnote
+    roof["modes"] = modes
+    return roof
+
+
+def make_step(args, rank, local):
+    """(step, sync, roofline_fn) for one replica. The stub (CPU launcher test) sleeps instead."""
+    if args.stub_step_ms is not None:
+        return (lambda: time.sleep(args.stub_step_ms / 1e3)), (lambda: None), None
+
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
     from spotter_amd import ops
     from spotter_amd.config import PRESETS
     from spotter_amd.engine import Engine
     from spotter_amd.synthetic import synthetic_batch
-    from spotter_amd.replicas import barrier, max_over_ranks
     from spotter_amd.weights import generate
 
     cfg = PRESETS[args.preset].replace(image_size=args.size)
@@ -248,24 +377,55 @@ def main():
         logits, pred = eng.forward(px)
         ops.postprocess(logits, pred, tsz, K, 0.5, scores, labels, boxes, counts, work)
 
+    step.cfg, step.weights = cfg, weights
+    return step, torch.cuda.synchronize, ops.set_launch_hook
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_replicas(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("SPOTTER_REPLICA_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    if args.gpus > 1 and world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+    from spotter_amd.replicas import all_gather_obj, barrier, max_over_ranks
+
+    step, sync, set_hook = make_step(args, rank, local)
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
 
-    rec = None if args.no_events else KernelEventRecorder(torch)
-    ops.set_launch_hook(rec)
+    rec = None
+    if set_hook is not None and not args.no_events:
+        import torch
+
+        rec = KernelEventRecorder(torch)
+        set_hook(rec)
 
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     t1 = time.perf_counter()
     barrier()
-    ops.set_launch_hook(None)
-    elapsed = t1 - t0
-    elapsed = max_over_ranks(elapsed)
+    if set_hook is not None:
+        set_hook(None)
+    mine = t1 - t0
+    elapsed = max_over_ranks(mine)
+    B = args.batch
+    per_rank = all_gather_obj({"rank": rank, "device": os.environ.get("HIP_VISIBLE_DEVICES", str(local)),
+                               "value": round(B * args.steps / mine, 2),
+                               "ms_per_step": round(1000 * mine / args.steps, 3)})
     n_img = world * B * args.steps
     value = n_img / elapsed
 
@@ -284,64 +444,22 @@ def main():
             classes[kind] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                              "frac": round(ach / peak, 4), "ms_per_step": round(c["busy"] / args.steps, 3),
                              "launches_per_step": c["n"] // args.steps}
-        c = cl["conv"]
-        per_launch_ms = c["ms"] / c["n"]
-        ach = c["flops"] / (c["busy"] * 1e-3) / 1e12
-        alg_bytes = c["bytes"] / c["n"]
-        traffic, tnote = load_traffic(args, alg_bytes)
-        if args.precision == "fp32-mfma":
-            kname = "conv_gemm_kernel (fp32 v_mfma_f32_32x32x2f32 implicit GEMM)"
-        elif bf:
-            kname = ("conv_glds_kernel<PL=1> (bf16 operands, v_mfma_f32_32x32x16_bf16 implicit GEMM, LDS-DMA staged; "
-                     + ("decoder linears f32x3)" if args.precision == "bf16" else "decoder linears bf16)"))
-        else:
-            kname = ("conv_glds_kernel<PL=3> (fp32 operands split hi/mid/lo bf16, 6 v_mfma_f32_32x32x16_bf16 "
-                     "per 32x32x16 block, implicit GEMM, LDS-DMA staged) + conv_gemm_kernel (fp32 "
-                     "v_mfma_f32_32x32x2f32) on thin layers and decoder linears; split in 'modes'")
-        roof = {"bound": "mfma", "kernel": kname,
-                "achieved": round(ach, 2), "peak": conv_peak, "unit": "TFLOP/s",
-                "frac": round(ach / conv_peak, 4), "traffic": traffic,
-                "launches_per_step": c["n"] // args.steps, "avg_launch_ms": round(per_launch_ms, 4),
-                "gflop_per_launch": round(c["flops"] / c["n"] / 1e9, 3),
-                "algorithmic_bytes_per_launch": int(alg_bytes),
-                "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2),
-                "conv_busy_ms_per_step": round(c["busy"] / args.steps, 3),
-                "note": "achieved = algorithmic conv/linear FLOPs / wall time with >=1 conv_gemm launch in flight "
-                        "(HIP events on the launch streams); traffic = HBM bytes per conv launch from PMC "
-                        "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
-        if tnote:
-            roof["traffic_source"] = tnote
-        # per operand mode: share of the class's FLOPs and time, and the matrix pipe's own instruction rate
-        # (the fp32-accurate split issues 6 bf16 MFMAs per fp32 32x32x16 product block)
-        modes = {}
-        per_mfma = {"x3": (6, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
-                    "bf16": (1, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
-                    "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS),
-                    "direct": (1, "v_fma_f32 (VALU stem conv, no MFMA)", FP32_MFMA_PEAK_TFLOPS)}
-        for md, c in rec.conv_modes().items():
-            a = c["flops"] / (c["ms"] * 1e-3) / 1e12
-            mult, instr, pk = per_mfma[md]
-            modes[md] = {"flop_share": round(c["flops"] / max(1, cl["conv"]["flops"]), 4),
-                         "ms_per_step": round(c["ms"] / args.steps, 3), "launches_per_step": c["n"] // args.steps,
-                         "achieved": round(a, 2), "unit": "TFLOP/s",
-                         "mfma_issue": {"instr": instr, "mfma_per_fp32_block": mult,
-                                        "achieved": round(mult * a, 1), "peak": pk, "frac": round(mult * a / pk, 4)}}
-        roof["modes"] = modes
+        roof = conv_roofline(rec, cl, args, bf)
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:
             json.dump(rec.by_shape(), f, indent=1)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.stub_step_ms is None:
         try:
-            cpu = cpu_baseline(cfg, weights, args.cpu_baseline_seconds)
+            cpu = cpu_baseline(step.cfg, step.weights, args.cpu_baseline_seconds, args.cpu_baseline_batch)
         except Exception as e:  # keep the GPU line even if the host path is unavailable
             cpu = {"value": None, "unit": "images/sec", "cores": None, "kind": "reference",
                    "sample": f"unavailable: {type(e).__name__}: {e}"}
 
     lat = None
-    if rank == 0 and world == 1 and args.latency_iters > 0:
+    if rank == 0 and world == 1 and args.latency_iters > 0 and args.stub_step_ms is None:
         try:
             from tools.latency import measure
 
@@ -350,6 +468,7 @@ def main():
             lat = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
+        S = args.size
         line = {
             "metric": (BASELINE_METRIC if (args.preset, S, B, args.precision) == ("r101vd", 640, 32, "fp32")
                        else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B} {args.precision}"),
@@ -360,12 +479,16 @@ def main():
             "config": {"workload": f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess",
                        "model": f"rtdetr_v2_{args.preset}", "global_batch": B * world, "image_size": S,
                        "parallelism": f"replicas x{world}"},
+            "per_rank": per_rank,
             "roofline": roof, "kernel_classes": classes, "cpu_baseline": cpu, "latency": lat,
         }
+        if args.stub_step_ms is not None:
+            line["data"] = "STUB: no GPU step (launcher test)"
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

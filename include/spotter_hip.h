@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 6
+#define SP_ABI_VERSION 7
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -122,6 +122,10 @@ int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int out_w, flo
                      void* stream);
 
 int sp_conv2d(const sp_conv_desc* d, void* stream);
+/* Test / tuning hook (ABI v7): force the GEMM tile configuration of later sp_conv2d calls made by
+ * the CALLING THREAD (-1, the default, = chosen by shape). Nothing on the product path calls it, and
+ * no environment variable is read: the production tile choice cannot be changed from outside. */
+int sp_set_conv_config(int cfg);
 
 /* NCHW → NHWC (pixel_values layout of the processor contract → conv layout). */
 int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* stream);

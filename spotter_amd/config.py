@@ -39,6 +39,7 @@ class SpotterConfig:
     hidden_sizes: list = field(default_factory=lambda: [256, 512, 1024, 2048])
     layer_type: str = "bottleneck"
     embedding_size: int = 64
+    hidden_act: str = "relu"  # backbone convs (RN:85-99, 168, 223)
     # hybrid encoder
     encoder_hidden_dim: int = 384
     encoder_ffn_dim: int = 2048
@@ -46,17 +47,22 @@ class SpotterConfig:
     encoder_in_channels: list = field(default_factory=lambda: [512, 1024, 2048])
     feat_strides: list = field(default_factory=lambda: [8, 16, 32])
     hidden_expansion: float = 1.0
-    positional_encoding_temperature: float = 10000.0
+    positional_encoding_temperature: int = 10000
+    encoder_activation_function: str = "gelu"  # AIFI FFN (M2:853)
+    activation_function: str = "silu"  # CCFM conv-norm layers (M2:915, 937, 1140, 1156)
+    eval_size: tuple | None = None  # set: AIFI runs without the sine position embedding (M2:1073-1081)
     # decoder
     d_model: int = 256
     decoder_in_channels: list = field(default_factory=lambda: [384, 384, 384])
     decoder_ffn_dim: int = 1024
+    decoder_activation_function: str = "relu"  # decoder FFN (M2:358)
     decoder_layers: int = 6
     decoder_attention_heads: int = 8
     decoder_n_levels: int = 3
     decoder_n_points: int = 4
     decoder_offset_scale: float = 0.5
     num_queries: int = 300
+    anchor_image_size: tuple | None = None  # set: anchors from this size / feat_strides (M2:1384, 1451-1456)
     num_labels: int = 80
     layer_norm_eps: float = 1e-5
     batch_norm_eps: float = 1e-5
@@ -75,7 +81,7 @@ class SpotterConfig:
         return dict(
             backbone=dict(depths=list(self.depths), hidden_sizes=list(self.hidden_sizes),
                           layer_type=self.layer_type, embedding_size=self.embedding_size,
-                          out_indices=[2, 3, 4]),
+                          hidden_act=self.hidden_act, out_indices=[2, 3, 4]),
             model=dict(encoder_hidden_dim=self.encoder_hidden_dim,
                        encoder_ffn_dim=self.encoder_ffn_dim,
                        encoder_in_channels=list(self.encoder_in_channels),
@@ -83,7 +89,18 @@ class SpotterConfig:
                        hidden_expansion=self.hidden_expansion,
                        decoder_layers=self.decoder_layers, d_model=self.d_model,
                        decoder_ffn_dim=self.decoder_ffn_dim, num_queries=self.num_queries,
-                       num_labels=self.num_labels, id2label=dict(self.id2label)),
+                       num_labels=self.num_labels, id2label=dict(self.id2label),
+                       encoder_attention_heads=self.encoder_attention_heads,
+                       decoder_attention_heads=self.decoder_attention_heads,
+                       decoder_n_points=self.decoder_n_points, decoder_offset_scale=self.decoder_offset_scale,
+                       feat_strides=list(self.feat_strides),
+                       positional_encoding_temperature=int(self.positional_encoding_temperature),
+                       layer_norm_eps=self.layer_norm_eps, batch_norm_eps=self.batch_norm_eps,
+                       encoder_activation_function=self.encoder_activation_function,
+                       activation_function=self.activation_function,
+                       decoder_activation_function=self.decoder_activation_function,
+                       eval_size=list(self.eval_size) if self.eval_size else None,
+                       anchor_image_size=list(self.anchor_image_size) if self.anchor_image_size else None),
         )
 
     def to_json(self) -> str:

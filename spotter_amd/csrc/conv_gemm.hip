@@ -21,8 +21,6 @@
 // BatchNorm scale/shift (FrozenBN M2:748-758 / eval BN), residual, activation,
 // post-activation residual, and a grouped output row map so projections write
 // straight into concatenated / flattened buffers (M2:1553-1555).
-#include <cstdlib>
-
 #include "conv_common.h"
 
 namespace sp {
@@ -261,12 +259,11 @@ int launch(const ConvArgs& a, hipStream_t s) {
   return launch_splitk_reduce(a, s);
 }
 
-// Tile override for tuning: SP_CONV_CFG = "<TM><TN><DB>" (fp32 kernel, e.g. "221") or the
-// conv_mfma16 config number (bf16 / split kernels).
-int forced_cfg() {
-  const char* e = getenv("SP_CONV_CFG");
-  return e ? atoi(e) : -1;
-}
+// Tile override for tests and tuning tools, set explicitly per thread by sp_set_conv_config (never
+// from the environment): "<TM><TN><DB>" for the fp32 kernel (e.g. 221) or the conv_mfma16 config
+// number (bf16 / split kernels); -1 = by shape (the production choice).
+thread_local int g_forced_cfg = -1;
+int forced_cfg() { return g_forced_cfg; }
 
 }  // namespace
 
@@ -279,6 +276,11 @@ int launch_splitk_reduce(const ConvArgs& a, hipStream_t s) {
 }
 
 }  // namespace sp
+
+extern "C" int sp_set_conv_config(int cfg) {
+  sp::g_forced_cfg = cfg < 0 ? -1 : cfg;
+  return 0;
+}
 
 extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   using namespace sp;

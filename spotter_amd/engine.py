@@ -40,10 +40,7 @@ def _t(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)
 
 
-def bf16_bits(a: np.ndarray) -> np.ndarray:
-    """fp32 → bf16 bit patterns, round to nearest even (weights are finite)."""
-    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
-    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack time)
 
 
 # precision → (conv GEMM operand mode, linear GEMM operand mode):
@@ -68,11 +65,12 @@ def _wkw(wq):
 
 
 class ConvW:
-    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16")
+    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16", "host")
 
-    def __init__(self, w, cin, cout, k, scale, shift, w16=None):
+    def __init__(self, w, cin, cout, k, scale, shift, w16=None, host=None):
         self.w, self.cin, self.cout, self.k, self.scale, self.shift = w, cin, cout, k, scale, shift
         self.w16 = w16
+        self.host = host  # the packed fp32 [Cout, K] weights on the host (pack-time fusions read them)
 
 
 class LinW:
@@ -144,6 +142,11 @@ class Engine:
         self.fold_repvgg = fold_repvgg
         self.fuse_shortcut = fuse_shortcut  # bottleneck tail + projection shortcut as one GEMM (_fused_tail)
         self.precision = precision
+        # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
+        self.act_bb = cfg.hidden_act
+        self.act_enc = cfg.activation_function
+        self.act_aifi = cfg.encoder_activation_function
+        self.act_dec = cfg.decoder_activation_function
         self._conv_mode, self._lin_mode = PRECISIONS[precision]
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
@@ -159,19 +162,21 @@ class Engine:
         self._consts = {}
         self._ctxs = {}
         self._outs = {}
-        self.microbatches = 2
+        # one stream: the measured fastest at bs32 (profiles/r1/microbatch_ab.json); k > 1 slices on
+        # k streams stay available as Engine.forward(microbatches=k)
+        self.microbatches = 1
         self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
     # ------------------------------------------------------------------ weights
-    @staticmethod
-    def _wq(w: torch.Tensor, mode: str):
-        """GEMM operand form of fp32 device weights w [Cout, K]: None (fp32 MFMA), bf16 bit
-        patterns (RNE), or the hi / mid / lo bf16 planes of the fp32-accurate split path."""
+    def _wq(self, w: np.ndarray, mode: str):
+        """GEMM operand form of host fp32 weights w [Cout, K], uploaded: None (fp32 MFMA), bf16 bit
+        patterns (RNE), or the hi / mid / lo bf16 planes of the fp32-accurate split path. The
+        rounding runs in numpy at pack time; the device only receives bit patterns."""
         if mode == "f32":
             return None
         if mode == "bf16":
-            return w.to(torch.bfloat16).view(torch.int16).contiguous()
-        return ops.split_bf16x3(w)
+            return torch.from_numpy(bf16_bits(w).view(np.int16)).to(self.dev)
+        return torch.from_numpy(ops.split_bf16x3_host(w)).to(self.dev)
 
     def _pick(self, mode: str, cout: int, kdim: int, small_m: bool = False) -> str:
         """Per-layer GEMM mode. Under precision "fp32" both operand modes are fp32-accurate, so layers
@@ -185,14 +190,15 @@ class Engine:
         return mode
 
     def _mk_conv(self, wk, ci, co, k, sc, sh):
-        w = _t(wk, self.dev)
-        return ConvW(w, ci, co, k, _t(sc, self.dev), _t(sh, self.dev),
-                     self._wq(w, self._pick(self._conv_mode, co, ci * k * k)))
+        wk = np.ascontiguousarray(wk, dtype=np.float32)
+        return ConvW(_t(wk, self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev),
+                     self._wq(wk, self._pick(self._conv_mode, co, ci * k * k)), host=wk)
 
     def _conv(self, p, conv_key, bn_pre, frozen):
         w = p[conv_key]
         co, ci, k, _ = w.shape
-        sc, sh = (frozen_bn_affine if frozen else eval_bn_affine)(p, bn_pre)
+        # FrozenBN's eps is fixed at 1e-5 (M2:755); the encoder's nn.BatchNorm2d uses config.batch_norm_eps
+        sc, sh = frozen_bn_affine(p, bn_pre) if frozen else eval_bn_affine(p, bn_pre, self.cfg.batch_norm_eps)
         return self._mk_conv(conv_khwc(w), ci, co, k, sc, sh)
 
     def _lin(self, p, pre, *more, per_query: bool = False):
@@ -203,7 +209,7 @@ class Engine:
         b = np.concatenate(bs, 0)
         wd = _t(w, self.dev)
         mode = self._pick(self._lin_mode, w.shape[0], w.shape[1], small_m=per_query and w.shape[0] > 128)
-        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(wd, mode))
+        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(w.astype(np.float32), mode))
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -294,12 +300,15 @@ class Engine:
         return self._mk_conv(wf.astype(np.float32), kc, co, 1, np.ones(co, np.float32), shift.astype(np.float32))
 
     def _csp(self, p, pre):
-        c1 = self._conv(p, pre + ".conv1.conv.weight", pre + ".conv1.norm", False)
-        c2 = self._conv(p, pre + ".conv2.conv.weight", pre + ".conv2.norm", False)
-        w12 = torch.cat([c1.w, c2.w], 0).contiguous()
-        c12 = ConvW(w12, c1.cin, c1.cout + c2.cout, 1,
-                    torch.cat([c1.scale, c2.scale]).contiguous(), torch.cat([c1.shift, c2.shift]).contiguous(),
-                    self._wq(w12, self._conv_mode))
+        # conv1 ‖ conv2: one GEMM over the same input (M2:949-951), concatenated on the host
+        w1 = p[pre + ".conv1.conv.weight"]
+        w2 = p[pre + ".conv2.conv.weight"]
+        s1, b1 = eval_bn_affine(p, pre + ".conv1.norm", self.cfg.batch_norm_eps)
+        s2, b2 = eval_bn_affine(p, pre + ".conv2.norm", self.cfg.batch_norm_eps)
+        w12 = np.concatenate([conv_khwc(w1), conv_khwc(w2)], 0)
+        c12 = ConvW(_t(w12, self.dev), w1.shape[1], w1.shape[0] + w2.shape[0], 1,
+                    _t(np.concatenate([s1, s2]), self.dev), _t(np.concatenate([b1, b2]), self.dev),
+                    self._wq(w12, self._conv_mode), host=w12)
         reps = []
         for b in range(3):
             q = f"{pre}.bottlenecks.{b}"
@@ -307,8 +316,8 @@ class Engine:
                 # RepVGG re-parameterisation (M2:921-923): BN1(conv3x3(x)) + BN2(conv1x1(x)) is one 3×3
                 # conv whose weights are s1·W3 with s2·W1 added to the centre tap, shift b1 + b2.
                 w3, w1 = p[q + ".conv1.conv.weight"], p[q + ".conv2.conv.weight"]
-                s1, b1 = eval_bn_affine(p, q + ".conv1.norm")
-                s2, b2 = eval_bn_affine(p, q + ".conv2.norm")
+                s1, b1 = eval_bn_affine(p, q + ".conv1.norm", self.cfg.batch_norm_eps)
+                s2, b2 = eval_bn_affine(p, q + ".conv2.norm", self.cfg.batch_norm_eps)
                 wf = (w3.astype(np.float64) * s1[:, None, None, None]).copy()
                 wf[:, :, 1, 1] += w1[:, :, 0, 0].astype(np.float64) * s2[:, None]
                 co, ci = w3.shape[:2]
@@ -321,7 +330,7 @@ class Engine:
         c3 = None
         if (pre + ".conv3.conv.weight") in p:
             c3 = self._conv(p, pre + ".conv3.conv.weight", pre + ".conv3.norm", False)
-        return {"c12": c12, "hid": c1.cout, "reps": reps, "c3": c3}
+        return {"c12": c12, "hid": w1.shape[0], "reps": reps, "c3": c3}
 
     # ------------------------------------------------------------------ workspace
     def _buf(self, key, *shape, dtype=torch.float32):
@@ -357,7 +366,7 @@ class Engine:
         """The stem's first conv (Cin 3, K = 27) runs on the direct NCHW kernel (sp_stem_conv3x3s2_nchw)
         in the fp32-weight modes; the bf16 variants keep it on the GEMM path with their rounding."""
         c = self.stem[0]
-        return c.cin == 3 and c.k == 3 and c.cout in (32, 64) and c.w16 is None
+        return c.cin == 3 and c.k == 3 and c.cout in (32, 64) and c.w16 is None and self.act_bb in ("relu", None)
 
     def backbone(self, pixel_values: torch.Tensor, B, H, W):
         """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC).
@@ -369,13 +378,13 @@ class Engine:
         s2 = self._buf("stem2", B, h1, w1, e)
         c0 = self.stem[0]
         if self._direct_stem():
-            ops.stem_conv_nchw(pixel_values, c0.w, c0.scale, c0.shift, view(s0, e // 2), c0.cout, act="relu")
+            ops.stem_conv_nchw(pixel_values, c0.w, c0.scale, c0.shift, view(s0, e // 2), c0.cout, act=self.act_bb)
         else:
             px = self._buf("px_nhwc", B, H, W, 3)
             ops.nchw_to_nhwc(pixel_values, px)
-            self._cv(view(px, 3), B, H, W, c0, 2, view(s0, e // 2), act="relu")
-        self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act="relu")
-        self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act="relu")
+            self._cv(view(px, 3), B, H, W, c0, 2, view(s0, e // 2), act=self.act_bb)
+        self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act=self.act_bb)
+        self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act=self.act_bb)
         h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
         b0 = self.blocks[0]
         if "fused" in b0 and b0["sc"] == "conv":
@@ -408,9 +417,9 @@ class Engine:
                     cat = cur
                 t1 = self._buf(f"s{s}_t1", B, h, w, red)
                 out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
-                self._cv(curv, B, h, w, L[0], 1, view(t1, red), act="relu")
-                self._cv(view(t1, red), B, h, w, L[1], st, V(cat, 0, kc), act="relu")
-                self._cv(V(cat, 0, kc), B, ho, wo, blk["fused"], 1, view(out, cout), act="relu")
+                self._cv(curv, B, h, w, L[0], 1, view(t1, red), act=self.act_bb)
+                self._cv(view(t1, red), B, h, w, L[1], st, V(cat, 0, kc), act=self.act_bb)
+                self._cv(V(cat, 0, kc), B, ho, wo, blk["fused"], 1, view(out, cout), act=self.act_bb)
                 curv, h, w, c = view(out, cout), ho, wo, cout
                 yield
                 continue
@@ -431,13 +440,13 @@ class Engine:
                 red = L[0].cout
                 t1 = self._buf(f"s{s}_t1", B, h, w, red)
                 t2 = self._buf(f"s{s}_t2", B, ho, wo, red)
-                self._cv(view(cur, c), B, h, w, L[0], 1, view(t1, red), act="relu")
-                self._cv(view(t1, red), B, h, w, L[1], st, view(t2, red), act="relu")
-                self._cv(view(t2, red), B, ho, wo, L[2], 1, view(out, cout), act="relu", res1=res)
+                self._cv(view(cur, c), B, h, w, L[0], 1, view(t1, red), act=self.act_bb)
+                self._cv(view(t1, red), B, h, w, L[1], st, view(t2, red), act=self.act_bb)
+                self._cv(view(t2, red), B, ho, wo, L[2], 1, view(out, cout), act=self.act_bb, res1=res)
             else:
                 t1 = self._buf(f"s{s}_t1", B, ho, wo, cout)
-                self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act="relu")
-                self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act="relu", res1=res)
+                self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act=self.act_bb)
+                self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act=self.act_bb, res1=res)
             curv, h, w, c = view(out, cout), ho, wo, cout
             yield
         feats.append((curv.t, h, w, c))
@@ -447,7 +456,7 @@ class Engine:
         """RTDetrV2CSPRepLayer.forward M2:948-952 on a 2·H-channel NHWC input."""
         hid = cs["hid"]
         c12 = self._buf(f"{tag}_c12", B, h, w, 2 * hid)
-        self._cv(x, B, h, w, cs["c12"], 1, view(c12, 2 * hid), act="silu")
+        self._cv(x, B, h, w, cs["c12"], 1, view(c12, 2 * hid), act=self.act_enc)
         h2 = V(c12, hid, 2 * hid)
         cur = V(c12, 0, 2 * hid)
         t = None if self.fold_repvgg else self._buf(f"{tag}_t", B, h, w, hid)
@@ -459,13 +468,13 @@ class Engine:
             else:
                 dst = view(self._buf(f"{tag}_r{b % 2}", B, h, w, hid), hid)
             if k3 == "fold":
-                self._cv(cur, B, h, w, k1, 1, dst, act="silu", res2=h2 if last else None)
+                self._cv(cur, B, h, w, k1, 1, dst, act=self.act_enc, res2=h2 if last else None)
             else:
                 self._cv(cur, B, h, w, k3, 1, view(t, hid))
-                self._cv(cur, B, h, w, k1, 1, dst, act="silu", res1=view(t, hid), res2=h2 if last else None)
+                self._cv(cur, B, h, w, k1, 1, dst, act=self.act_enc, res1=view(t, hid), res2=h2 if last else None)
             cur = dst
         if cs["c3"] is not None:
-            self._cv(cur, B, h, w, cs["c3"], 1, out, act="silu")
+            self._cv(cur, B, h, w, cs["c3"], 1, out, act=self.act_enc)
 
     def encoder(self, feats, B):
         """encoder_input_proj (M2:1512) + RTDetrV2HybridEncoder.forward (M2:1164-1209)."""
@@ -494,34 +503,35 @@ class Engine:
         ff = self._buf("aifi_ff", rows, cfg.encoder_ffn_dim)
         t2 = self._buf("aifi_t2", rows, Hd)
         p5a = self._buf("p5a", rows, Hd)
-        self._lin_op(view(p5, Hd), rows, A["qk"], view(qk, 2 * Hd), a2=view(pos, Hd))
+        # with config.eval_size set HF runs AIFI without the position embedding (M2:1073-1081)
+        self._lin_op(view(p5, Hd), rows, A["qk"], view(qk, 2 * Hd), a2=None if cfg.eval_size else view(pos, Hd))
         self._lin_op(view(p5, Hd), rows, A["v"], view(vv, Hd))
         heads = cfg.encoder_attention_heads
         ops.attention(V(qk, 0, 2 * Hd), V(qk, Hd, 2 * Hd), view(vv, Hd), view(at, Hd), B, n, heads, Hd // heads,
                       (Hd // heads) ** -0.5)
         self._lin_op(view(at, Hd), rows, A["o"], view(t1, Hd), res1=view(p5, Hd))
         ops.layernorm(view(t1, Hd), *A["ln1"], view(y1, Hd), rows, Hd, cfg.layer_norm_eps)
-        self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act="gelu")
+        self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act=self.act_aifi)
         self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(t2, Hd), res1=view(y1, Hd))
         ops.layernorm(view(t2, Hd), *A["ln2"], view(p5a, Hd), rows, Hd, cfg.layer_norm_eps)
         yield
         # FPN (M2:1183-1197)
-        self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act="silu")
+        self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act=self.act_enc)
         ops.upsample2x(V(catn5, Hd, 2 * Hd), V(cat4, 0, 2 * Hd), B, h2, w2, Hd)
         F4 = self._buf("F4", B, h1, w1, Hd)
         self._csp_fwd(self.fpn[0], view(cat4, 2 * Hd), B, h1, w1, view(F4, Hd), "fpn0")
         yield
-        self._cv(view(F4, Hd), B, h1, w1, self.lateral[1], 1, V(catn4, Hd, 2 * Hd), act="silu")
+        self._cv(view(F4, Hd), B, h1, w1, self.lateral[1], 1, V(catn4, Hd, 2 * Hd), act=self.act_enc)
         ops.upsample2x(V(catn4, Hd, 2 * Hd), V(cat3, 0, 2 * Hd), B, h1, w1, Hd)
         F3 = self._buf("F3", B, h0, w0, Hd)
         self._csp_fwd(self.fpn[1], view(cat3, 2 * Hd), B, h0, w0, view(F3, Hd), "fpn1")
         yield
         # PAN (M2:1199-1207)
-        self._cv(view(F3, Hd), B, h0, w0, self.down[0], 2, V(catn4, 0, 2 * Hd), act="silu")
+        self._cv(view(F3, Hd), B, h0, w0, self.down[0], 2, V(catn4, 0, 2 * Hd), act=self.act_enc)
         N4 = self._buf("N4", B, h1, w1, Hd)
         self._csp_fwd(self.pan[0], view(catn4, 2 * Hd), B, h1, w1, view(N4, Hd), "pan0")
         yield
-        self._cv(view(N4, Hd), B, h1, w1, self.down[1], 2, V(catn5, 0, 2 * Hd), act="silu")
+        self._cv(view(N4, Hd), B, h1, w1, self.down[1], 2, V(catn5, 0, 2 * Hd), act=self.act_enc)
         N5 = self._buf("N5", B, h2, w2, Hd)
         self._csp_fwd(self.pan[1], view(catn5, 2 * Hd), B, h2, w2, view(N5, Hd), "pan1")
         return [(F3, h0, w0), (N4, h1, w1), (N5, h2, w2)]
@@ -634,6 +644,12 @@ class Engine:
         cfg = self.cfg
         D, Q, NC = cfg.d_model, cfg.num_queries, cfg.num_labels
         # query selection (M2:1582-1623)
+        if cfg.anchor_image_size:
+            # fixed anchors from config.anchor_image_size (M2:1384, 1451-1456); HF cannot combine them with
+            # feature maps of another size either
+            ashapes = [(int(cfg.anchor_image_size[0] / s), int(cfg.anchor_image_size[1] / s)) for s in cfg.feat_strides]
+            if [tuple(s) for s in ashapes] != [tuple(s) for s in shapes]:
+                raise ValueError(f"anchor_image_size {cfg.anchor_image_size} gives levels {ashapes}, input has {shapes}")
         anchors, valid = self._const(("anchors", tuple(shapes)), lambda: tuple(
             _t(a, self.dev) for a in anchors_for(shapes)))
         rows = B * S
@@ -689,7 +705,7 @@ class Engine:
             self._lin_op(view(at, D), Bq, P["out"], view(tmp, D), res1=view(h, D))
             ops.layernorm(view(tmp, D), *P["ln2"], view(h, D), Bq, D, cfg.layer_norm_eps)
             # FFN (M2:426-429)
-            self._lin_op(view(h, D), Bq, P["fc1"], view(ff, cfg.decoder_ffn_dim), act="relu")
+            self._lin_op(view(h, D), Bq, P["fc1"], view(ff, cfg.decoder_ffn_dim), act=self.act_dec)
             self._lin_op(view(ff, cfg.decoder_ffn_dim), Bq, P["fc2"], view(tmp, D), res1=view(h, D))
             ops.layernorm(view(tmp, D), *P["ln3"], view(h, D), Bq, D, cfg.layer_norm_eps)
             # iterative box refinement (M2:636-639)

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 from ._lib import SpConvDesc, SpImageU8, SpMsdaDesc, call
@@ -148,15 +149,39 @@ def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=No
                   res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes)
 
 
+def bf16_bits(a) -> np.ndarray:
+    """fp32 → bf16 bit patterns (uint16), round to nearest even (finite inputs; weights are)."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def _bf16_float(bits: np.ndarray) -> np.ndarray:
+    return (bits.astype(np.uint32) << 16).view(np.float32)
+
+
+def split_bf16x3_host(w) -> np.ndarray:
+    """fp32 weights (host) → int16 [3, numel] bf16 bit planes hi, mid, lo with w == hi + mid + lo
+    (RNE at each step; both residuals are exact in fp32): the operand format of SP_PREC_F32X3.
+    Host numpy at weight-pack time: no device arithmetic outside the HIP kernels."""
+    w = np.ascontiguousarray(w, dtype=np.float32).reshape(-1)
+    hi = bf16_bits(w)
+    r1 = w - _bf16_float(hi)
+    mid = bf16_bits(r1)
+    lo = bf16_bits(r1 - _bf16_float(mid))
+    return np.stack([hi, mid, lo]).view(np.int16)
+
+
 def split_bf16x3(w: torch.Tensor) -> torch.Tensor:
-    """fp32 weights → int16 [3, numel] bf16 bit planes hi, mid, lo with w == hi + mid + lo
-    (RNE at each step; both residuals are exact in fp32), the operand format of SP_PREC_F32X3."""
-    w = w.detach().float().reshape(-1)
-    hi = w.to(torch.bfloat16)
-    r1 = w - hi.float()
-    mid = r1.to(torch.bfloat16)
-    lo = (r1 - mid.float()).to(torch.bfloat16)
-    return torch.stack([hi, mid, lo]).view(torch.int16).contiguous()
+    """split_bf16x3_host of a (device) fp32 tensor, uploaded to the tensor's device (tests / tools)."""
+    return torch.from_numpy(split_bf16x3_host(w.detach().cpu().numpy())).to(w.device)
+
+
+def force_conv_config(cfg=None):
+    """Tests / tuning tools: pin the GEMM tile configuration of this thread's later conv2d calls
+    (sp_set_conv_config); None restores the by-shape production choice."""
+    from ._lib import lib
+
+    lib().sp_set_conv_config(-1 if cfg in (None, "", "-") else int(cfg))
 
 
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):

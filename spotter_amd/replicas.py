@@ -32,6 +32,17 @@ def max_over_ranks(x: float) -> float:
     return float(t.item())
 
 
+def all_gather_obj(obj) -> list:
+    """Every rank's `obj` (rank order) over the gloo control group; [obj] without one."""
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def barrier():
     import torch.distributed as dist
 

@@ -22,6 +22,15 @@ def dev():
     return torch.device("cuda", 0)
 
 
+@pytest.fixture(autouse=True)
+def _reset_conv_config():
+    """A test that pins a tile configuration (sp_set_conv_config) leaves the by-shape choice behind."""
+    yield
+    from spotter_amd import ops
+
+    ops.force_conv_config(None)
+
+
 def T(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
@@ -92,8 +101,10 @@ def test_conv2d_matches_oracle(dev, case, workspace=None):
 @pytest.mark.parametrize("cfg", ["220", "221", "210", "211", "120", "121", "110", "111",
                                  "4110", "4111", "4210", "4211", "4120", "4121"])
 def test_conv2d_every_tile_config(dev, cfg, monkeypatch):
-    """Each tile variant (SP_CONV_CFG override) on a ragged 3×3 and a 1×1 with residuals."""
-    monkeypatch.setenv("SP_CONV_CFG", cfg)
+    """Each tile variant (sp_set_conv_config override) on a ragged 3×3 and a 1×1 with residuals."""
+    from spotter_amd import ops
+
+    ops.force_conv_config(cfg)
     for case in [(2, 11, 9, 64, 136, 3, 1, "silu"), (1, 7, 13, 96, 72, 1, 1, "relu"), (1, 9, 9, 3, 32, 3, 2, None),
                  (2, 13, 11, 32, 32, 3, 1, "relu")]:
         test_conv2d_matches_oracle(dev, case)
@@ -124,7 +135,7 @@ def test_conv2d_bf16_matches_bf16_rounded_reference(dev, case, cfg, monkeypatch)
     from spotter_amd.ops import view
 
     if cfg:
-        monkeypatch.setenv("SP_CONV_CFG", cfg)
+        ops.force_conv_config(cfg)
     n, h, w, cin, cout, k, st, act = case
     rng = np.random.default_rng(hash(case) % 2**32 + 1)
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
@@ -181,12 +192,12 @@ def test_conv2d_f32x3_is_fp32_accurate(dev, case, cfg, monkeypatch):
     outs = {}
     for mode in ("fp32", "f32x3"):
         if mode == "f32x3" and cfg:
-            monkeypatch.setenv("SP_CONV_CFG", cfg)
+            ops.force_conv_config(cfg)
         out = torch.empty(m * cout, device=dev)
         ops.conv2d(xd, n, h, w, cin, wk, cout, k, st, pad, view(out, cout), workspace=ws,
                    wt_planes=ops.split_bf16x3(wk) if mode == "f32x3" else None)
         outs[mode] = out.cpu().numpy().reshape(m, cout).astype(np.float64)
-        monkeypatch.delenv("SP_CONV_CFG", raising=False)
+        ops.force_conv_config(None)
     scale = np.abs(ref).max()
     e32 = np.abs(outs["fp32"] - ref).max()
     ex3 = np.abs(outs["f32x3"] - ref).max()
@@ -287,6 +298,27 @@ def test_pools_into_channel_slice(dev):
     xt = T(x.reshape(-1), dev)
     for fn, ref, (ho, wo) in ((ops.maxpool3x3s2, maxpool3s2, ((h - 1) // 2 + 1, (w - 1) // 2 + 1)),
                               (ops.avgpool2x2_ceil, avgpool2_ceil, ((h + 1) // 2, (w + 1) // 2))):
+        y = torch.full((n * ho * wo * (red + c),), 7.0, device=dev)
+        fn(xt, V(y, red, red + c), n, h, w, c)
+        got = y.cpu().numpy().reshape(n, ho, wo, red + c)
+        np.testing.assert_allclose(got[..., red:], ref(x), rtol=1e-6, atol=1e-6)
+        assert np.all(got[..., :red] == 7.0)
+
+
+def test_pools_past_65535_output_rows(dev):
+    """n·ho > 65535 output rows: the pools clamp gridDim.y and stride over rows (elementwise.hip), here
+    with 66000 rows (n = 33000, h = 3), into a channel slice of a wider buffer."""
+    from oracle.rtdetr_np import avgpool2_ceil, maxpool3s2
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(9)
+    n, h, w, c, red = 33000, 3, 2, 4, 4
+    x = rng.standard_normal((n, h, w, c)).astype(np.float32)
+    xt = T(x.reshape(-1), dev)
+    for fn, ref, (ho, wo) in ((ops.maxpool3x3s2, maxpool3s2, ((h - 1) // 2 + 1, (w - 1) // 2 + 1)),
+                              (ops.avgpool2x2_ceil, avgpool2_ceil, ((h + 1) // 2, (w + 1) // 2))):
+        assert n * ho > 65535
         y = torch.full((n * ho * wo * (red + c),), 7.0, device=dev)
         fn(xt, V(y, red, red + c), n, h, w, c)
         got = y.cpu().numpy().reshape(n, ho, wo, red + c)

@@ -119,3 +119,127 @@ def test_checkpoint_key_renames():
     assert rename_key("model.decoder.layers.0.self_attn.out_proj.weight") == "model.decoder.layers.0.self_attn.o_proj.weight"
     assert rename_key("model.decoder.layers.3.fc1.bias") == "model.decoder.layers.3.mlp.fc1.bias"
     assert rename_key("model.encoder.encoder.0.layers.0.fc2.weight") == "model.encoder.aifi.0.layers.0.mlp.fc2.weight"
+
+
+def test_bench_launcher_spawns_one_replica_per_gpu():
+    """bench.py --gpus 2 (no torch.distributed launcher) spawns two replica processes, each pinned to
+    its own device by HIP_VISIBLE_DEVICES, that meet only in the gloo barrier / max.
+    The GPU step is stubbed (a sleep), so this runs on the CPU."""
+    import json
+    import sys
+
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--stub-step-ms", "20"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["global_batch"] == 64
+    assert [p["rank"] for p in line["per_rank"]] == [0, 1]
+    assert [p["device"] for p in line["per_rank"]] == ["0", "1"]
+    # whole-job value = both replicas' images over the max elapsed (each ~32 img / 20 ms)
+    assert 2 * 32 / 0.040 < line["value"] <= 2 * 32 / 0.020 * 1.01
+
+
+@pytest.mark.parametrize("preset", ["r18vd", "r101vd"])
+def test_config_from_hf_reads_hf_config_json(preset, tmp_path):
+    """config.json as HF itself writes it (RTDetrV2Config.save_pretrained) → the same SpotterConfig as the
+    preset; our own writer (checkpoint.hf_config_dict) is read back identically; no field is unknown."""
+    import dataclasses
+    import json
+
+    from transformers import RTDetrResNetConfig, RTDetrV2Config
+
+    from spotter_amd.checkpoint import config_from_hf, hf_config_dict, unknown_fields
+    from spotter_amd.config import PRESETS
+
+    cfg = PRESETS[preset]
+    kw = cfg.to_hf_kwargs()
+    RTDetrV2Config(backbone_config=RTDetrResNetConfig(**kw["backbone"]), **kw["model"]).save_pretrained(tmp_path)
+    js = json.loads((tmp_path / "config.json").read_text())
+    assert unknown_fields(js) == []
+    got = dataclasses.asdict(config_from_hf(js))
+    want = dataclasses.asdict(cfg)
+    assert {k: (got[k], want[k]) for k in got if k != "name" and got[k] != want[k]} == {}
+    assert dataclasses.asdict(config_from_hf(hf_config_dict(cfg))) == got
+
+
+@pytest.mark.parametrize("field,value", [("decoder_method", "discrete"), ("normalize_before", True),
+                                         ("encoder_activation_function", "tanh"), ("learn_initial_query", True),
+                                         ("decoder_n_points", [4, 4, 4]), ("num_feature_levels", 4),
+                                         ("use_focal_loss", False)])
+def test_config_from_hf_refuses_unimplemented_values(field, value):
+    from spotter_amd.checkpoint import UnsupportedConfig, config_from_hf, hf_config_dict
+    from spotter_amd.config import PRESETS
+
+    js = hf_config_dict(PRESETS["r18vd"])
+    js[field] = value
+    with pytest.raises(UnsupportedConfig):
+        config_from_hf(js)
+    js = hf_config_dict(PRESETS["r18vd"])
+    js["backbone_config"]["hidden_act"] = "tanh"
+    with pytest.raises(UnsupportedConfig):
+        config_from_hf(js)
+
+
+def test_config_from_hf_reads_nondefault_supported_values():
+    """Supported non-default values are carried, not dropped (activations, eps, eval / anchor sizes)."""
+    from spotter_amd.checkpoint import config_from_hf, hf_config_dict
+    from spotter_amd.config import PRESETS
+
+    js = hf_config_dict(PRESETS["r18vd"])
+    js.update(encoder_activation_function="relu", activation_function="gelu", decoder_activation_function="silu",
+              layer_norm_eps=1e-6, batch_norm_eps=1e-3, eval_size=[640, 640], anchor_image_size=[640, 640],
+              positional_encoding_temperature=20)
+    c = config_from_hf(js)
+    assert (c.encoder_activation_function, c.activation_function, c.decoder_activation_function) == ("relu", "gelu", "silu")
+    assert (c.layer_norm_eps, c.batch_norm_eps, c.eval_size, c.anchor_image_size) == (1e-6, 1e-3, (640, 640), (640, 640))
+    assert c.positional_encoding_temperature == 20
+
+
+def test_local_checkpoint_round_trip(tmp_path):
+    """save_local writes config.json + model.safetensors with 4.x key names (the inverse of
+    conversion_mapping.py:1042-1047); load_local maps them back to exactly the generated tensors."""
+    from safetensors.numpy import load_file
+
+    from spotter_amd.checkpoint import load_local, save_local
+    from spotter_amd.config import PRESETS
+    from spotter_amd.weights import generate
+
+    cfg = PRESETS["r18vd"]
+    w = generate(cfg, seed=3)
+    save_local(str(tmp_path), cfg, w)
+    raw = load_file(str(tmp_path / "model.safetensors"))
+    assert any(".out_proj." in k for k in raw) and not any(".o_proj." in k for k in raw)
+    assert any(".layers.0.fc1." in k for k in raw) and not any(".mlp.fc" in k for k in raw)
+    assert any(k.startswith("model.encoder.encoder.0.layers.0.") for k in raw)
+    cfg2, w2 = load_local(str(tmp_path))
+    assert cfg2.depths == cfg.depths and cfg2.encoder_hidden_dim == cfg.encoder_hidden_dim
+    assert set(w2) == set(w)
+    assert all(np.array_equal(w2[k], w[k]) for k in w)
+
+
+def test_weight_split_on_host_matches_torch_rne():
+    """ops.split_bf16x3_host / bf16_bits (numpy, pack time) against torch's own RNE bf16 cast on the CPU:
+    hi / mid / lo bit-identical to the chained casts, and hi + mid + lo == w exactly."""
+    import torch
+
+    from spotter_amd import ops
+
+    rng = np.random.default_rng(0)
+    w = np.concatenate([rng.standard_normal(4096).astype(np.float32) * 10.0 ** rng.integers(-8, 8, 4096),
+                        np.array([0.0, -0.0, 1.0, 1 + 2 ** -8, 1 + 2 ** -9, 3e-39, 65504.0])]).astype(np.float32)
+    planes = ops.split_bf16x3_host(w).view(np.uint16)
+    t = torch.from_numpy(w)
+    hi = t.to(torch.bfloat16)
+    r1 = t - hi.float()
+    mid = r1.to(torch.bfloat16)
+    lo = (r1 - mid.float()).to(torch.bfloat16)
+    for got, ref in zip(planes, (hi, mid, lo)):
+        assert np.array_equal(got, ref.view(torch.int16).numpy().view(np.uint16))
+    f = [(p.astype(np.uint32) << 16).view(np.float32).astype(np.float64) for p in planes]
+    normal = (np.abs(w) >= 1e-30) | (w == 0)  # far enough from the subnormal range for lo to stay exact
+    assert np.array_equal((f[0] + f[1] + f[2])[normal], w.astype(np.float64)[normal])

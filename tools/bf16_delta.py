@@ -23,27 +23,17 @@ def iou(a, b):
     return inter / ua if ua > 0 else 0.0
 
 
-def delta(preset, tag=None, precision="bf16"):
-    from tests.test_gpu_model import load_images
-    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
-    from spotter_amd.config import PRESETS
-    from spotter_amd.engine import Engine
-
-    g = np.load(os.path.join(GOLD, f"{tag or preset + '_640'}.npz"))
-    size = int(g["size"])
-    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)
-    model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision)
-    proc = SpotterImageProcessor(size={"height": size, "width": size})
-    off = 0
+def match_stats(dets, g):
+    """Detection agreement of per-image `dets` (post_process dicts, image i ↔ golden image i % n) with
+    the fp32 goldens: same label and IoU >= 0.5, |Δscore| of the matched pairs."""
+    n_gold = len(g["det_counts"])
+    starts = np.concatenate([[0], np.cumsum(g["det_counts"])]).astype(int)
     tot = dict(expected=0, matched=0, extra=0, max_dscore=0.0, max_dbox_px=0.0)
     ds = []
-    for i, img in enumerate(load_images(g)):
-        out = model(**proc(images=img))
-        th, tw = g["target_sizes"][i]
-        det = proc.post_process_object_detection(out, target_sizes=torch.tensor([[th, tw]]), threshold=0.5)[0]
-        n = int(g["det_counts"][i])
-        es, el, eb = g["det_scores"][off:off + n], g["det_labels"][off:off + n], g["det_boxes"][off:off + n]
-        off += n
+    for i, det in enumerate(dets):
+        gi = i % n_gold
+        a, b_ = starts[gi], starts[gi + 1]
+        es, el, eb = g["det_scores"][a:b_], g["det_labels"][a:b_], g["det_boxes"][a:b_]
         used = set()
         for s, l, b in zip(es, el, eb):
             best, bi = 0.0, -1
@@ -59,12 +49,31 @@ def delta(preset, tag=None, precision="bf16"):
                 ds.append(abs(float(det["scores"][bi]) - float(s)))
                 tot["max_dscore"] = max(tot["max_dscore"], ds[-1])
                 tot["max_dbox_px"] = max(tot["max_dbox_px"], float(np.abs(det["boxes"][bi].numpy() - b).max()))
-        tot["expected"] += n
+        tot["expected"] += len(es)
         tot["extra"] += len(det["scores"]) - len(used)
     tot["recall_vs_fp32"] = tot["matched"] / max(1, tot["expected"])
     tot["p50_dscore"] = float(np.percentile(ds, 50)) if ds else 0.0
     tot["p95_dscore"] = float(np.percentile(ds, 95)) if ds else 0.0
     return tot
+
+
+def delta(preset, tag=None, precision="bf16"):
+    from tests.test_gpu_model import load_images
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+
+    g = np.load(os.path.join(GOLD, f"{tag or preset + '_640'}.npz"))
+    size = int(g["size"])
+    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)
+    model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision)
+    proc = SpotterImageProcessor(size={"height": size, "width": size})
+    dets = []
+    for i, img in enumerate(load_images(g)):
+        out = model(**proc(images=img))
+        th, tw = g["target_sizes"][i]
+        dets.append(proc.post_process_object_detection(out, target_sizes=torch.tensor([[th, tw]]), threshold=0.5)[0])
+    return match_stats(dets, g)
 
 
 if __name__ == "__main__":

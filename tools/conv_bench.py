@@ -2,7 +2,7 @@
 
     python tools/conv_bench.py [--prec fp32,f32x3,bf16] [--cfgs -,1,2] [--shapes 0,1,2] [--reps 20]
 
-cfg "-" = the library's own tile choice; other values go to SP_CONV_CFG (fp32 kernel: "<TM><TN><DB>",
+cfg "-" = the library's own tile choice; other values go to sp_set_conv_config (fp32 kernel: "<TM><TN><DB>",
 bf16 / f32x3 kernels: 1..6). Prints one JSON line per (shape, precision, cfg), plus the step-weighted
 total for the default choice.
 """
@@ -54,10 +54,7 @@ SHAPES = [
 
 def bench_one(dev, shape, prec, cfg, reps, ws=False):
     n, h, w, cin, cout, k, st, act, resid, _ = shape
-    if cfg and cfg != "-":
-        os.environ["SP_CONV_CFG"] = cfg
-    else:
-        os.environ.pop("SP_CONV_CFG", None)
+    ops.force_conv_config(cfg)
     pad = k // 2
     ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
     m = n * ho * wo

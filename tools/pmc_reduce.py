@@ -32,10 +32,27 @@ def read(path, counter):
     return rows
 
 
+def operand_planes(short: str):
+    """bf16 operand planes of a conv_mfma16.hip kernel instance from its template arguments
+    (3 = the fp32-accurate split 'x3' kernels, 1 = bf16); None for other kernels."""
+    import re
+
+    m = re.search(r"(conv_glds_kernel|conv_mfma16_kernel|conv_pipe_kernel|conv_pp_kernel)<([^>]*)>", short)
+    if not m:
+        return None
+    args = [a.strip() for a in m.group(2).split(",")]
+    pos = 2 if m.group(1) == "conv_pp_kernel" else 4
+    return int(args[pos]) if len(args) > pos and args[pos].isdigit() else None
+
+
 def fold(rows):
     out = {}
     for name, v in rows:
         short = name.replace("(anonymous namespace)", "").split("(")[0]
+        if operand_planes(short) == 3:  # the dominant kernel, broken out (it also counts under conv)
+            c = out.setdefault("conv_x3", {"kib": 0.0, "n": 0})
+            c["kib"] += v
+            c["n"] += 1
         for cls, keys in CLASSES:
             if any(k in short for k in keys):
                 c = out.setdefault(cls, {"kib": 0.0, "n": 0})

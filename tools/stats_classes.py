@@ -6,6 +6,7 @@ average conv launch duration must agree).
 """
 import csv
 import json
+import os
 import sys
 
 CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "stem_conv")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
@@ -34,8 +35,15 @@ def main(path, csv_out=None):
             w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs"])
             for n, c, t in sorted(rs, key=lambda r: -r[2]):
                 w.writerow([n, c, int(t), round(t / c, 1)])
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pmc_reduce import operand_planes
+
     for name, calls, total_ns in rs:
         short = name.replace("(anonymous namespace)", "").split("(")[0]
+        if operand_planes(short) == 3:  # the dominant kernel's own class (also counted under conv)
+            c = out.setdefault("conv_x3", {"calls": 0, "total_ms": 0.0})
+            c["calls"] += calls
+            c["total_ms"] += total_ns / 1e6
         cls = next((c for c, keys in CLASSES if any(k in short for k in keys)), "other")
         c = out.setdefault(cls, {"calls": 0, "total_ms": 0.0})
         c["calls"] += calls
