@@ -1150,7 +1150,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51)) && !a.d.A2) {
+  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 60 && cfg <= 64)) && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
       case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
@@ -1178,10 +1178,15 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       // 64-wide N (Cout = 64 layers): 4 waves of 64×64 stacked along M
       case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
       case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
+      // one A row band per wave, the full N width: every A fragment split once per workgroup
+      case 60: return launch_glds<8, 1, 1, 8, 2>(a, planes, s);      // 256×256, 8 waves of 32×256
+      case 62: return launch_glds<4, 1, 1, 8, 2>(a, planes, s);      // 128×256, 4 waves of 32×256
+      case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
+      case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || cfg > 51 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 60) || cfg > 64 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

@@ -74,6 +74,10 @@ class SpotterForObjectDetection:
 
             cfg, weights = load_local(name_or_path)
             return cls(cfg, weights)
+        import warnings
+
+        warnings.warn(f"{name_or_path!r} is not a local checkpoint directory (nothing is fetched): using the "
+                      f"{_preset_for(name_or_path).name} preset with deterministic SYNTHETIC weights", stacklevel=2)
         return cls(_preset_for(name_or_path), None, seed=kw.get("seed", 0))
 
     def _host_weights(self):

@@ -243,3 +243,55 @@ def test_weight_split_on_host_matches_torch_rne():
     f = [(p.astype(np.uint32) << 16).view(np.float32).astype(np.float64) for p in planes]
     normal = (np.abs(w) >= 1e-30) | (w == 0)  # far enough from the subnormal range for lo to stay exact
     assert np.array_equal((f[0] + f[1] + f[2])[normal], w.astype(np.float64)[normal])
+
+
+def test_rayservice_template_renders():
+    """deploy/rayservice-template.yaml rendered as spotter-manager renders the reference template
+    (Go text/template, the single action {{.DockerImage}}, handlers.go:98-118) and decoded as YAML
+    (handlers.go:124-150): GVR ray.io/v1alpha1 (handlers.go:152-156), one Serve replica per MI355X."""
+    import yaml
+
+    src = open(os.path.join(ROOT, "deploy", "rayservice-template.yaml")).read()
+    body = "\n".join(l for l in src.splitlines() if not l.lstrip().startswith("#"))
+    assert re.findall(r"{{[^}]*}}", body) and set(re.findall(r"{{[^}]*}}", body)) == {"{{.DockerImage}}"}
+    image = "registry.local/spotter-mi355x:test"
+    doc = yaml.safe_load(body.replace("{{.DockerImage}}", image))
+    assert doc["apiVersion"] == "ray.io/v1alpha1" and doc["kind"] == "RayService"
+    assert doc["metadata"]["name"] == "spotter-ray-service"
+    serve = yaml.safe_load(doc["spec"]["serveConfigV2"])
+    app = serve["applications"][0]
+    assert (app["name"], app["import_path"], app["route_prefix"]) == ("spotter-serve", "spotter.serve:deployment", "/detect")
+    dep = app["deployments"][0]
+    assert dep["name"] == "AmenitiesDetector" and dep["ray_actor_options"]["num_gpus"] == 1
+    rc = doc["spec"]["rayClusterConfig"]
+    head = rc["headGroupSpec"]["template"]["spec"]["containers"][0]
+    assert head["image"] == image and rc["headGroupSpec"]["rayStartParams"]["num-gpus"] == "0"
+    (wg,) = rc["workerGroupSpecs"]
+    worker = wg["template"]["spec"]["containers"][0]
+    assert worker["image"] == image
+    gpus = worker["resources"]["limits"]["amd.com/gpu"]
+    assert worker["resources"]["requests"]["amd.com/gpu"] == gpus
+    assert int(wg["rayStartParams"]["num-gpus"]) == gpus == dep["num_replicas"] == 8
+    env = {e["name"]: e["value"] for e in worker["env"]}
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["MODEL_NAME"].startswith("/models/")
+
+
+def test_dockerfile_copies_exist_in_their_contexts():
+    """deploy/Dockerfile.rocm builds from the spotter repo root (as the reference apps/spotter/Dockerfile)
+    plus this repo as the named context `spotter_amd`: every COPY source exists in its context."""
+    ref = "/root/reference"
+    lines = open(os.path.join(ROOT, "deploy", "Dockerfile.rocm")).read().splitlines()
+    copies = [l.split()[1:] for l in lines if l.startswith("COPY ")]
+    assert copies
+    for args in copies:
+        frm = next((a.split("=", 1)[1] for a in args if a.startswith("--from=")), None)
+        srcs = [a for a in args if not a.startswith("--")][:-1]
+        for s in srcs:
+            if frm == "spotter_amd":
+                assert os.path.exists(os.path.join(ROOT, s)), s
+            elif frm == "checkpoint":
+                assert s == "/"
+            elif os.path.isdir(ref):  # the spotter repo root, when present in this container
+                assert os.path.exists(os.path.join(ref, s)), s
+    stages = [l.split()[-1] for l in lines if l.startswith("FROM ")]
+    assert {"checkpoint", "spotter_amd"} <= set(stages)
