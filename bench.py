@@ -461,9 +461,14 @@ def main():
     lat = None
     if rank == 0 and world == 1 and args.latency_iters > 0 and args.stub_step_ms is None:
         try:
+            from spotter_amd import SpotterForObjectDetection
+            from spotter_amd.config import PRESETS
+            from tools import detect_path
             from tools.latency import measure
 
-            lat = measure(args.preset, args.latency_iters, graphs=True)
+            lat_model = SpotterForObjectDetection(PRESETS[args.preset], use_graphs=True)
+            lat = measure(args.preset, args.latency_iters, graphs=True, model=lat_model)
+            lat["full_request"] = detect_path.measure(args.preset, args.latency_iters, model=lat_model)
         except Exception as e:
             lat = {"error": f"{type(e).__name__}: {e}"}
 

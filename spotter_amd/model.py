@@ -51,8 +51,15 @@ class SpotterForObjectDetection:
     main_input_name = "pixel_values"
 
     def __init__(self, cfg: SpotterConfig, weights: dict | None = None, seed: int = 0,
-                 use_graphs: bool = True, precision: str = "fp32"):
+                 use_graphs: bool = True, precision: str = "fp32", batching: bool = False,
+                 max_batch: int = 32, max_wait_ms: float = 2.0):
+        """batching: coalesce concurrent calls (several request threads) into one engine forward
+        (spotter_amd.batching.MicroBatcher, up to max_batch images within max_wait_ms)."""
         self.cfg = cfg
+        self.batching = batching
+        self.max_batch = max_batch
+        self.max_wait_ms = max_wait_ms
+        self._batcher = None
         self.use_graphs = use_graphs
         self.precision = precision  # engine.PRECISIONS key; "fp32" = the fp32-accurate parity path
         self._graphs = {}
@@ -73,12 +80,12 @@ class SpotterForObjectDetection:
             from .checkpoint import load_local
 
             cfg, weights = load_local(name_or_path)
-            return cls(cfg, weights)
+            return cls(cfg, weights, **{k: v for k, v in kw.items() if k != "seed"})
         import warnings
 
         warnings.warn(f"{name_or_path!r} is not a local checkpoint directory (nothing is fetched): using the "
                       f"{_preset_for(name_or_path).name} preset with deterministic SYNTHETIC weights", stacklevel=2)
-        return cls(_preset_for(name_or_path), None, seed=kw.get("seed", 0))
+        return cls(_preset_for(name_or_path), None, **kw)
 
     def _host_weights(self):
         if self._weights is None:
@@ -100,6 +107,7 @@ class SpotterForObjectDetection:
     def __getstate__(self):
         st = self.__dict__.copy()
         st["_engine"] = None
+        st["_batcher"] = None
         st["_lock"] = None
         st["_graphs"] = {}
         st["_seen"] = set()
@@ -128,6 +136,15 @@ class SpotterForObjectDetection:
         eng = self.engine
         if torch.is_tensor(pixel_values) and pixel_values.device != eng.dev:
             pixel_values = pixel_values.to(eng.dev)
+        if getattr(self, "batching", False):
+            if self._batcher is None:
+                with self._lock:
+                    if self._batcher is None:
+                        from .batching import MicroBatcher
+
+                        self._batcher = MicroBatcher(eng.forward, eng.dev, self.max_batch, self.max_wait_ms)
+            logits, boxes = self._batcher(pixel_values.float())
+            return SpotterDetectionOutput(logits=logits, pred_boxes=boxes)
         key = tuple(pixel_values.shape)
         if self.use_graphs and key[0] <= 4:
             # small batches are launch-bound: replay a captured hipGraph of the whole forward

@@ -260,3 +260,41 @@ def test_from_pretrained_local_checkpoint_matches_hf_goldens(tmp_path):
     model.use_graphs = False
     assert model.cfg.depths == [3, 4, 23, 3]
     run_case("r101vd", model=model)
+
+
+def test_request_microbatching_matches_single_calls():
+    """F3: 12 request threads calling the drop-in model at bs1 concurrently are served by fewer engine
+    forwards (spotter_amd.batching), and each gets its own image's outputs (vs the bs1 eager path:
+    split-K summation order only, so at the parity bar)."""
+    import threading
+
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.synthetic import synthetic_image
+
+    cfg = PRESETS["r18vd"]
+    ref_model = SpotterForObjectDetection(cfg, use_graphs=False)
+    model = SpotterForObjectDetection(cfg, batching=True, max_batch=8, max_wait_ms=20)
+    model._weights = ref_model._host_weights()
+    proc = SpotterImageProcessor()
+    imgs = [synthetic_image(300 + i) for i in range(12)]
+    ref = [torch.sigmoid(ref_model(**proc(images=im)).logits[0]).cpu().numpy() for im in imgs]
+    model(**proc(images=imgs[0]))  # engine + batcher up
+    got = [None] * 12
+    barrier = threading.Barrier(12)
+
+    def call(i):
+        x = proc(images=imgs[i])
+        barrier.wait()
+        with torch.no_grad():
+            got[i] = torch.sigmoid(model(**x).logits[0]).cpu().numpy()
+
+    th = [threading.Thread(target=call, args=(i,)) for i in range(12)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    b = model._batcher
+    assert b.images == 13 and b.batches < 13, (b.batches, b.images)
+    for i in range(12):
+        np.testing.assert_allclose(np.sort(got[i].max(-1)), np.sort(ref[i].max(-1)), rtol=0, atol=SCORE_TOL)

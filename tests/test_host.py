@@ -295,3 +295,103 @@ def test_dockerfile_copies_exist_in_their_contexts():
                 assert os.path.exists(os.path.join(ref, s)), s
     stages = [l.split()[-1] for l in lines if l.startswith("FROM ")]
     assert {"checkpoint", "spotter_amd"} <= set(stages)
+
+
+def test_detect_path_harness_with_fake_model():
+    """tools/detect_path.py (the whole-/detect latency harness) on the CPU with a fake processor/model:
+    real HTTP fetch, decode, label filter, draw, JPEG + base64, response JSON."""
+    import asyncio
+    import base64
+    import io
+    import json
+    import sys
+
+    import httpx
+    import torch
+    from PIL import Image
+
+    sys.path.insert(0, ROOT)
+    from tools import detect_path
+
+    class Proc:
+        def __call__(self, images, return_tensors="pt"):
+            class B(dict):
+                def to(self, d):
+                    return self
+            return B(pixel_values=torch.zeros(1, 3, 8, 8))
+
+        def post_process_object_detection(self, outputs, target_sizes, threshold):
+            return [{"scores": torch.tensor([0.9, 0.8]), "labels": torch.tensor([62, 65]),
+                     "boxes": torch.tensor([[10.0, 20.0, 110.0, 220.0], [1.0, 2.0, 3.0, 4.0]])}]
+
+    class Cfg:
+        id2label = {62: "tv", 65: "remote"}
+
+    class Model:
+        config = Cfg()
+
+        def __call__(self, **kw):
+            return None
+
+    jpeg = open(os.path.join(ROOT, "tests", "golden", "test_pic.jpg"), "rb").read()
+    srv, url = detect_path.serve_bytes(jpeg)
+
+    async def run():
+        async with httpx.AsyncClient() as client:
+            return await detect_path.handle(json.dumps({"image_urls": [url]}).encode(), client, Proc(), Model(), {})
+
+    try:
+        out = json.loads(asyncio.run(run()))
+    finally:
+        srv.shutdown()
+    assert out["amenities_description"] == "The property contains: TV."
+    (img,) = out["images"]
+    assert img["detections"] == [{"label": "TV", "box": [10.0, 20.0, 110.0, 220.0]}]
+    with Image.open(io.BytesIO(base64.b64decode(img["labeled_image_base64"]))) as im:
+        assert im.size == (1200, 717)
+
+
+def test_microbatcher_coalesces_concurrent_calls():
+    """spotter_amd.batching on the CPU with a fake engine: 16 concurrent threads' bs1 calls run as a
+    few batched forwards, every caller gets its own rows, mixed image sizes never share a batch,
+    and a failing forward reaches every caller of that batch."""
+    import threading
+
+    import torch
+
+    from spotter_amd.batching import MicroBatcher
+
+    seen = []
+
+    def run(x):
+        seen.append(tuple(x.shape))
+        time.sleep(0.01)
+        return x[:, 0, 0, :1].repeat(1, 3).unsqueeze(-1), x[:, 0, :4, 0].unsqueeze(1)
+
+    import time
+    mb = MicroBatcher(run, "cpu", max_batch=8, max_wait_ms=20)
+    res = {}
+
+    def caller(i):
+        s = 8 if i % 4 else 16
+        x = torch.full((1, 3, s, s), float(i))
+        res[i] = mb(x)
+
+    th = [threading.Thread(target=caller, args=(i,)) for i in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert all(float(res[i][0].flatten()[0]) == i and res[i][0].shape == (1, 3, 1) for i in range(16))
+    assert mb.images == 16 and mb.batches < 16
+    assert all(b <= 8 for b, *_ in seen) and len({s[2] for s in seen if s[0] > 1}) <= 2
+    assert all(len({sh[2]}) == 1 for sh in seen)
+
+    def boom(x):
+        raise RuntimeError("kernel failed")
+
+    mb2 = MicroBatcher(boom, "cpu", max_batch=4, max_wait_ms=5)
+    with pytest.raises(RuntimeError, match="kernel failed"):
+        mb2(torch.zeros(1, 3, 8, 8))
+    mb.close()
+    mb2.close()
