@@ -1098,6 +1098,249 @@ int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
   return launch_splitk_reduce(a, s);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Staggered split-GEMM kernel (x3 / bf16): 8 waves, each owning 32 rows × the whole BN = 32·TN
+// columns of a 256 × BN tile, so every A fragment is split once per workgroup (VALU per MFMA
+// = 44 / (6·TN) instead of 44 / (6·TN) × the waves that share a row band). k advances 16 per LDS
+// stage, NS = 4 stages (fp32 A 16 KB + 3 bf16 B planes 24 KB each). Between two barriers a wave
+// does two independent things: the MFMAs of step t (A planes split in the previous interval,
+// B fragments read now) and the read + split of A for step t+1. Waves 0-3 split first, waves 4-7
+// compute first, so on every SIMD one wave's VALU / LDS work runs beside the other's MFMA chain
+// instead of both waves doing the same kind of work at the same time. DMA for step t+3 is issued
+// right after barrier t into the buffer step t-1 used; it has two intervals to land.
+template <int TN, int PL>
+__global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
+  constexpr int NT = 512, BM = 256, BN = 32 * TN, BK = 16, NS = 4;
+  constexpr int CA = BM * 4;   // 16-byte chunks of the fp32 A stage (4 per row)
+  constexpr int CB = 256 * 2;  // chunks of one bf16 B plane (2 per row; 256 rows, rows >= BN zero)
+  constexpr int GA = CA / NT;  // 2
+  constexpr int GLDS = GA + PL;
+  constexpr int STAGE = CA + PL * CB;
+  constexpr int EB = TN % 2 == 0 ? TN / 2 : TN;  // epilogue column blocks per round
+  constexpr int EPI = 8 * 32 * EB * 32 / 4;
+  constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
+  static_assert(SMEM * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[SMEM];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+
+  const int tilesN = (d.Cout + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int mt = wg / tilesN;
+  const int n0 = (wg - mt * tilesN) * BN;
+  const int64_t m0 = (int64_t)mt * BM;
+
+  // A pieces: tile row (j·NT + tid) / 4, LDS position tid % 4, global chunk (tid % 4) ^ ((row >> 2) & 3)
+  const int ca = (tid & 3) ^ ((tid >> 4) & 3);
+  int a_iy0[GA], a_ix0[GA];
+  const float* a_ptr[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int64_t m = m0 + ((j * NT + tid) >> 2);
+    const bool ok = m < p.M;
+    const int64_t mm = ok ? m : 0;
+    const int b = (int)(mm / p.HoWo);
+    const int rem = (int)(mm - (int64_t)b * p.HoWo);
+    const int oy = rem / d.Wo;
+    const int ox = rem - oy * d.Wo;
+    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
+    a_ix0[j] = ox * d.stride - d.pad;
+    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+  }
+  // B piece (one per plane): tile row tid / 2, global chunk (tid & 1) ^ ((row >> 3) & 1)
+  const int cbk = (tid & 1) ^ ((tid >> 4) & 1);
+  const int brow_ld = tid >> 1;
+  const bool b_ok = brow_ld < BN && n0 + brow_ld < d.Cout;
+  const uint16_t* b_ptr = d.Wt_bf16 + (int64_t)(b_ok ? n0 + brow_ld : 0) * p.K + cbk * 8;
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+
+  int s_kh = 0, s_kw = 0, s_c0 = 0;
+  const int nk_all = p.K / BK;
+  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
+  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
+  const int nk = kt1 - kt0;
+  {
+    const int k0 = kt0 * BK;
+    const int tap = k0 / d.Cin;
+    s_c0 = k0 - tap * d.Cin;
+    s_kh = tap / d.KW;
+    s_kw = tap - s_kh * d.KW;
+  }
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int kt, int buf) {
+    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
+      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
+      glds16(src, st + j * NT * 16);
+    }
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) {
+      const void* src = b_ok ? static_cast<const void*>(b_ptr + pl * wps + k0) : static_cast<const void*>(zero + cbk * 16);
+      glds16(src, st + (CA + pl * CB) * 16);
+    }
+    s_c0 += BK;
+    if (s_c0 >= d.Cin) {
+      s_c0 = 0;
+      if (++s_kw == d.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+  };
+
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int arow = wave * 32 + r;
+  const int apos0 = arow * 4 + ((2 * h) ^ ((arow >> 2) & 3));
+  const int apos1 = arow * 4 + ((2 * h + 1) ^ ((arow >> 2) & 3));
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+
+  bf16x8 fa[PL];  // A planes of the step whose MFMAs run next
+  bf16x8 fn[PL];  // A planes being prepared for the step after
+  auto split_a = [&](int buf, bf16x8* out) {
+    const uint4* st = smem + buf * STAGE;
+    const float4 x0 = *reinterpret_cast<const float4*>(st + apos0);
+    const float4 x1 = *reinterpret_cast<const float4*>(st + apos1);
+    split8<PL>(x0, x1, out);
+  };
+  auto mma = [&](int buf) {
+    const uint4* st = smem + buf * STAGE + CA;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int brow = j * 32 + r;
+      const int bpos = brow * 2 + (h ^ ((brow >> 3) & 1));
+      bf16x8 fb[PL];
+#pragma unroll
+      for (int pl = 0; pl < PL; ++pl) fb[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + bpos);
+      acc[j] = mfma_planes<PL>(fa, fb, acc[j]);
+    }
+  };
+
+  // prologue: steps 0..2 in flight, step 0 landed, its A planes split
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < nk) issue(kt0 + t, t);
+  if (nk > 0) {
+    if (nk >= 3) wait_vmcnt<2 * GLDS>();
+    else if (nk == 2) wait_vmcnt<GLDS>();
+    else wait_vmcnt<0>();
+    raw_barrier();
+    split_a(0, fa);
+  }
+  const bool first_split = wave < 4;
+  for (int t = 0; t < nk; ++t) {
+    // step t+1 landed (steps up to t+2 issued: one step may stay in flight)
+    if (t + 2 < nk) wait_vmcnt<GLDS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();  // everyone is past interval t-1: buffer (t-1) % 4 is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < nk) issue(kt0 + t + NS - 1, (t + NS - 1) % NS);
+    const bool more = t + 1 < nk;
+    if (first_split) {
+      if (more) split_a((t + 1) % NS, fn);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(t % NS);
+    } else {
+      mma(t % NS);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) split_a((t + 1) % NS, fn);
+    }
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) fa[pl] = fn[pl];
+  }
+
+  __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
+  float* region = reinterpret_cast<float*>(smem) + wave * (32 * EB * 32);
+  constexpr int W = EB * 32;
+  const sp_conv_desc& dd = p.d;
+  const bool fastv = p.vec_epi && p.splits == 1;
+  const int64_t mb = m0 + wave * 32;
+#pragma unroll
+  for (int j0 = 0; j0 < TN; j0 += EB) {
+    if (j0) __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int j = 0; j < EB; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) region[((q & 3) + 8 * (q >> 2) + 4 * h) * W + j * 32 + r] = acc[j0 + j][q];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    constexpr int PER = 32 * (W / 4) / 64;
+    constexpr int G = PER < 4 ? PER : 4;
+    static_assert(PER % G == 0, "task groups");
+    for (int t0 = 0; t0 < PER; t0 += G) {
+      float4 r1[G];
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int cidx = lane + 64 * (t0 + u);
+        const int row = cidx / (W / 4);
+        const int col = (cidx - row * (W / 4)) * 4;
+        const int64_t m = mb + row;
+        const int n = n0 + j0 * 32 + col;
+        r1[u] = (fastv && dd.res1 && m < p.M && n < dd.Cout) ? *reinterpret_cast<const float4*>(dd.res1 + m * dd.ldr1 + n)
+                                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < G; ++u) {
+        const int cidx = lane + 64 * (t0 + u);
+        const int row = cidx / (W / 4);
+        const int col = (cidx - row * (W / 4)) * 4;
+        const int64_t m = mb + row;
+        const int n = n0 + j0 * 32 + col;
+        if (m >= p.M || n >= dd.Cout) continue;
+        const float4 v = *reinterpret_cast<const float4*>(region + row * W + col);
+        if (p.splits > 1) {
+          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+        } else if (fastv) {
+          epilogue_vec(p, m, n, v, r1[u]);
+        } else {
+          epilogue_store(p, m, n, v);
+        }
+      }
+    }
+  }
+}
+
+template <int TN>
+int launch_x3s(const ConvArgs& a, int planes, hipStream_t s) {
+  if (a.d.Cin % 16 || a.K % 16) {
+    set_error("sp_conv2d: staggered kernel needs Cin %% 16 == 0 (Cin=%d)", a.d.Cin);
+    return -1;
+  }
+  constexpr int BN = 32 * TN;
+  const int64_t tiles = ((a.M + 255) / 256) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  dim3 grid((unsigned)tiles, 1, a.splits);
+  if (planes == 3)
+    hipLaunchKernelGGL((conv_x3s_kernel<TN, 3>), grid, dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_x3s_kernel<TN, 1>), grid, dim3(512), 0, s, a);
+  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 staggered)" : "sp_conv2d(bf16 staggered)");
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
+}
+
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
@@ -1134,6 +1377,13 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
+  if (cfg >= 70 && cfg <= 72 && !a.d.A2) {
+    switch (cfg) {
+      case 70: return launch_x3s<8>(a, planes, s);  // 256×256
+      case 71: return launch_x3s<6>(a, planes, s);  // 256×192
+      default: return launch_x3s<4>(a, planes, s);  // 256×128
+    }
+  }
   if (cfg >= 31 && cfg <= 32 && !a.d.A2) {
     switch (cfg) {
       case 31: return launch_pp<2, 2>(a, planes, s);  // 256×128, waves of 64×64
@@ -1150,7 +1400,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 60 && cfg <= 64)) && !a.d.A2) {
+  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 62 && cfg <= 64)) && !a.d.A2) {
     switch (cfg) {
       case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
       case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
@@ -1179,14 +1429,13 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
       case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
       // one A row band per wave, the full N width: every A fragment split once per workgroup
-      case 60: return launch_glds<8, 1, 1, 8, 2>(a, planes, s);      // 256×256, 8 waves of 32×256
       case 62: return launch_glds<4, 1, 1, 8, 2>(a, planes, s);      // 128×256, 4 waves of 32×256
       case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
       case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 60) || cfg > 64 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 72 || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes
