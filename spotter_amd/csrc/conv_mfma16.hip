@@ -1221,16 +1221,29 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
     const float4 x1 = *reinterpret_cast<const float4*>(st + apos1);
     split8<PL>(x0, x1, out);
   };
+  // B fragments double-buffered in registers: block j+1's ds_reads are issued before block j's
+  // MFMAs, so each wait covers loads issued one 6-MFMA group (192 cycles) earlier.
+  const int bpos0 = r * 2 + (h ^ ((r >> 3) & 1));  // (brow >> 3) & 1 is the same for brow = j·32 + r
   auto mma = [&](int buf) {
-    const uint4* st = smem + buf * STAGE + CA;
+    const uint4* st = smem + buf * STAGE + CA + bpos0;
+    bf16x8 fb[2][PL];
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) fb[0][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int brow = j * 32 + r;
-      const int bpos = brow * 2 + (h ^ ((brow >> 3) & 1));
-      bf16x8 fb[PL];
+      if (j + 1 < TN) {
 #pragma unroll
-      for (int pl = 0; pl < PL; ++pl) fb[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + bpos);
-      acc[j] = mfma_planes<PL>(fa, fb, acc[j]);
+        for (int pl = 0; pl < PL; ++pl)
+          fb[(j + 1) & 1][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + (j + 1) * 64);
+      }
+      acc[j] = mfma_planes<PL>(fa, fb[j & 1], acc[j]);
+    }
+    // issue order: block 0's ds_reads; then per block j the ds_reads of block j+1 ahead of j's MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, PL == 3 ? 6 : 1, 0);
     }
   };
 
