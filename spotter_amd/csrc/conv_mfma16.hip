@@ -35,6 +35,11 @@
 #ifndef SP_ABLATE
 #define SP_ABLATE 0
 #endif
+// conv_x3s_kernel ablation bits (timing experiments only; results are wrong with any bit set):
+// 1 no in-loop DMA, 2 no A split (raw bits), 4 no MFMA, 8 no in-loop barrier
+#ifndef SP_X3S_ABL
+#define SP_X3S_ABL 0
+#endif
 
 namespace sp {
 
@@ -1219,7 +1224,13 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
     const uint4* st = smem + buf * STAGE;
     const float4 x0 = *reinterpret_cast<const float4*>(st + apos0);
     const float4 x1 = *reinterpret_cast<const float4*>(st + apos1);
+#if SP_X3S_ABL & 2
+    bf16x8 raw = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(x0.x), __float_as_uint(x0.y),
+                                                       __float_as_uint(x1.x), __float_as_uint(x1.y)));
+    for (int q = 0; q < PL; ++q) out[q] = raw;
+#else
     split8<PL>(x0, x1, out);
+#endif
   };
   // B fragments double-buffered in registers: block j+1's ds_reads are issued before block j's
   // MFMAs, so each wait covers loads issued one 6-MFMA group (192 cycles) earlier.
@@ -1236,7 +1247,11 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
         for (int pl = 0; pl < PL; ++pl)
           fb[(j + 1) & 1][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + (j + 1) * 64);
       }
+#if SP_X3S_ABL & 4
+      for (int pl = 0; pl < PL; ++pl) asm volatile("" ::"v"(fa[pl]), "v"(fb[j & 1][pl]));
+#else
       acc[j] = mfma_planes<PL>(fa, fb[j & 1], acc[j]);
+#endif
     }
     // issue order: block 0's ds_reads; then per block j the ds_reads of block j+1 ahead of j's MFMAs
     __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
@@ -1264,9 +1279,13 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
     if (t + 2 < nk) wait_vmcnt<GLDS>();
     else wait_vmcnt<0>();
     __builtin_amdgcn_sched_barrier(0);
+#if !(SP_X3S_ABL & 8)
     raw_barrier();  // everyone is past interval t-1: buffer (t-1) % 4 is free
+#endif
     __builtin_amdgcn_sched_barrier(0);
+#if !(SP_X3S_ABL & 1)
     if (t + NS - 1 < nk) issue(kt0 + t + NS - 1, (t + NS - 1) % NS);
+#endif
     const bool more = t + 1 < nk;
     if (first_split) {
       if (more) split_a((t + 1) % NS, fn);
