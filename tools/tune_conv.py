@@ -1,0 +1,107 @@
+"""Per-shape GEMM tile tuning over the conv/linear shapes one bench step actually launches.
+
+    python tools/tune_conv.py <bench --detail JSON> [--out tune.json] [--reps 10] [--min-ms 0.05]
+
+Reads the per-shape timings `bench.py --detail` writes (shape key (M, Cout, K, k, stride, mode)),
+rebuilds each GEMM (1×1 / linear: one row of M pixels; 3×3: 32 square images), times every tile
+configuration its operand mode has (sp_set_conv_config) and records the fastest. The winners become
+spotter_amd/csrc/tile_table.h (tools/gen_tile_table.py), the exact-shape part of the tile choice.
+"""
+from __future__ import annotations
+
+import argparse
+import ast
+import json
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from spotter_amd import ops
+from spotter_amd.ops import view
+
+X3_CFGS = ["-", "11", "12", "13", "14", "16", "17", "33", "41", "44", "45", "46", "50", "51", "62", "63", "64",
+           "70", "71", "72"]
+F32_CFGS = ["-", "110", "111", "120", "121", "210", "211", "220", "221", "4110", "4111", "4210", "4120"]
+
+
+def geometry(m, cout, K, k, stride):
+    """(n, h, w, cin) of a GEMM with M = m rows: 1×1 convs and linears as one row of m pixels."""
+    cin = K // (k * k)
+    if k == 1 and stride == 1:
+        return 1, 1, m, cin
+    n = 32
+    ho = int(round(math.sqrt(m / n)))
+    if n * ho * ho != m:
+        n, ho = 1, int(round(math.sqrt(m)))
+    h = ho * stride
+    return n, h, h, cin
+
+
+def time_one(dev, m, cout, K, k, stride, mode, cfg, reps):
+    n, h, w, cin = geometry(m, cout, K, k, stride)
+    pad = k // 2
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(n * h * w * cin, device=dev, generator=g)
+    wt = torch.randn(cout * K, device=dev, generator=g) * (1.0 / K ** 0.5)
+    out = torch.empty(m * cout, device=dev)
+    kw = {"wt_planes": ops.split_bf16x3(wt)} if mode == "x3" else {}
+    ops.force_conv_config(None if cfg == "-" else cfg)
+
+    def run():
+        ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, stride, pad, view(out, cout), **kw)
+
+    try:
+        for _ in range(2):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
+    except RuntimeError:
+        return None
+    finally:
+        ops.force_conv_config(None)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("detail")
+    ap.add_argument("--out", default="tune.json")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--min-ms", type=float, default=0.05, help="skip shapes cheaper than this per step")
+    ap.add_argument("--steps", type=int, default=10, help="steps the detail file was recorded over")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    rows = json.load(open(a.detail))
+    res = []
+    for r in rows:
+        m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])
+        per_step = r["ms"] / a.steps
+        if mode not in ("x3", "f32") or per_step < a.min_ms:
+            continue
+        launches = r["launches"] / a.steps
+        times = {}
+        for cfg in (X3_CFGS if mode == "x3" else F32_CFGS):
+            t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps)
+            if t is not None:
+                times[cfg] = round(t, 4)
+        best = min(times, key=times.get)
+        e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "launches_per_step": launches,
+             "default_ms": times.get("-"), "best_cfg": best, "best_ms": times[best], "times": times,
+             "saving_ms_per_step": round((times.get("-", times[best]) - times[best]) * launches, 4)}
+        res.append(e)
+        print(json.dumps(e), flush=True)
+    tot = sum(e["saving_ms_per_step"] for e in res)
+    json.dump({"shapes": res, "saving_ms_per_step": round(tot, 3)}, open(a.out, "w"), indent=1)
+    print(json.dumps({"saving_ms_per_step": round(tot, 3)}))
+
+
+if __name__ == "__main__":
+    main()
