@@ -22,6 +22,7 @@
 // post-activation residual, and a grouped output row map so projections write
 // straight into concatenated / flattened buffers (M2:1553-1555).
 #include "conv_common.h"
+#include "tile_table.h"
 
 namespace sp {
 
@@ -349,9 +350,14 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     }
   }
   hipStream_t s = as_stream(stream);
-  if (planes) return launch_mfma16(a, planes, forced_cfg(), s);
+  // tile choice: a test / tuning override, else the measured exact-shape table (tile_table.h),
+  // else the by-shape rules below and in launch_mfma16
+  int cfg = forced_cfg();
+  if (cfg < 0 && a.splits == 1 && planes != 1)
+    cfg = tile_table_lookup(a.M, d->Cout, a.K, d->KH, d->stride, planes);
+  if (planes) return launch_mfma16(a, planes, cfg, s);
   if (a.splits > 1) return launch<1, 1, 0>(a, s);
-  switch (forced_cfg()) {
+  switch (cfg) {
     case 220: return launch<2, 2, 0>(a, s);
     case 221: return launch<2, 2, 1>(a, s);
     case 210: return launch<2, 1, 0>(a, s);
