@@ -25,6 +25,9 @@ inline int check_launch(const char* what) {
   return 0;
 }
 
+// compute units of the device sp_device_init selected (MI355X: 256); sizes persistent grids
+extern int g_num_cus;
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 constexpr int kWave = 64;

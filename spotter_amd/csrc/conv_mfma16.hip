@@ -1373,6 +1373,257 @@ int launch_x3s(const ConvArgs& a, int planes, hipStream_t s) {
   return launch_splitk_reduce(a, s);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Persistent staggered split-GEMM kernel (x3 / bf16). The x3s interval structure (8 waves × 32
+// rows × BN columns, k16 stages, 4-stage LDS ring, waves 0-3 split-then-MFMA, waves 4-7
+// MFMA-then-split), run by one workgroup per CU over a STREAM of (tile, k-step) pairs: the ring
+// never drains between tiles, so the next tile's first stages land while the current one
+// finishes, and there is no per-tile launch / prologue. The MFMAs compute Cᵀ (weights as the
+// first operand, activations as the second), which leaves every lane holding 4-channel groups
+// of one output pixel: the fused epilogue goes straight from registers to float4 loads / stores
+// (no LDS staging), so its stores drain while the next tile's MFMAs run.
+// Tiles are dealt XCD-major: the tiles of XCD x are a contiguous range, taken round-robin by the
+// workgroups on that XCD (N fastest), so concurrently running tiles share A row panels in L2.
+template <int TN, int PL>
+__global__ __launch_bounds__(512) void conv_x3p_kernel(const ConvArgs p, int ntiles) {
+  constexpr int NT = 512, BM = 256, BN = 32 * TN, BK = 16, NS = 4;
+  constexpr int CA = BM * 4;
+  constexpr int CB = 256 * 2;
+  constexpr int GA = CA / NT;
+  constexpr int GLDS = GA + PL;
+  constexpr int STAGE = CA + PL * CB;
+  static_assert(NS * STAGE * 16 <= 163840, "LDS");
+  __shared__ uint4 smem[NS * STAGE];
+
+  const sp_conv_desc& d = p.d;
+  const int64_t wps = d.wt_plane_stride;
+  const int tid = threadIdx.x;
+  const int wave = tid >> 6;
+  const int lane = tid & 63;
+  const int tilesN = (d.Cout + BN - 1) / BN;
+
+  // this workgroup's tiles: XCD-contiguous ranges, round-robin inside the XCD
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7;
+  const int loc = blockIdx.x >> 3;
+  const int nloc = (G - xcd + 7) >> 3;
+  const int t_beg = (int)((int64_t)ntiles * xcd / 8);
+  const int t_end = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  const int my_tiles = t_end - t_beg > loc ? (t_end - t_beg - loc + nloc - 1) / nloc : 0;
+  const int nk = p.K / BK;
+  const int total = my_tiles * nk;
+
+  const int ca = (tid & 3) ^ ((tid >> 4) & 3);
+  const int cbk = (tid & 1) ^ ((tid >> 4) & 1);
+  const int brow_ld = tid >> 1;
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+
+  // issue cursor: the tile / k-step the next DMA belongs to
+  int i_tile = 0, i_k = 0, s_kh = 0, s_kw = 0, s_c0 = 0;
+  int a_iy0[GA], a_ix0[GA];
+  const float* a_ptr[GA];
+  bool b_ok = false;
+  const uint16_t* b_ptr = nullptr;
+  auto set_issue_tile = [&](int ti) {
+    const int wg = t_beg + loc + ti * nloc;
+    const int mt = wg / tilesN;
+    const int n0 = (wg - mt * tilesN) * BN;
+    const int64_t m0 = (int64_t)mt * BM;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int64_t m = m0 + ((j * NT + tid) >> 2);
+      const bool ok = m < p.M;
+      const int64_t mm = ok ? m : 0;
+      const int b = (int)(mm / p.HoWo);
+      const int rem = (int)(mm - (int64_t)b * p.HoWo);
+      const int oy = rem / d.Wo;
+      const int ox = rem - oy * d.Wo;
+      a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
+      a_ix0[j] = ox * d.stride - d.pad;
+      a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+    }
+    b_ok = brow_ld < BN && n0 + brow_ld < d.Cout;
+    b_ptr = d.Wt_bf16 + (int64_t)(b_ok ? n0 + brow_ld : 0) * p.K + cbk * 8;
+    s_kh = s_kw = s_c0 = 0;
+  };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
+  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
+  auto issue = [&](int buf) {  // the cursor's k-step into stage `buf`, then advance the cursor
+    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
+      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
+      glds16(src, st + j * NT * 16);
+    }
+    const int k0 = i_k * BK;
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) {
+      const void* src = b_ok ? static_cast<const void*>(b_ptr + pl * wps + k0) : static_cast<const void*>(zero + cbk * 16);
+      glds16(src, st + (CA + pl * CB) * 16);
+    }
+    s_c0 += BK;
+    if (s_c0 >= d.Cin) {
+      s_c0 = 0;
+      if (++s_kw == d.KW) {
+        s_kw = 0;
+        ++s_kh;
+      }
+    }
+    if (++i_k == nk) {
+      i_k = 0;
+      if (++i_tile < my_tiles) set_issue_tile(i_tile);
+    }
+  };
+
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int arow = wave * 32 + r;
+  const int apos0 = arow * 4 + ((2 * h) ^ ((arow >> 2) & 3));
+  const int apos1 = arow * 4 + ((2 * h + 1) ^ ((arow >> 2) & 3));
+  const int bpos0 = r * 2 + (h ^ ((r >> 3) & 1));
+
+  f32x16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+
+  bf16x8 fa[PL], fn[PL];
+  auto split_a = [&](int buf, bf16x8* out) {
+    const uint4* st = smem + buf * STAGE;
+    const float4 x0 = *reinterpret_cast<const float4*>(st + apos0);
+    const float4 x1 = *reinterpret_cast<const float4*>(st + apos1);
+    split8<PL>(x0, x1, out);
+  };
+  auto mma = [&](int buf) {  // Cᵀ += W_j · Aᵀ for the 8 (TN) column blocks
+    const uint4* st = smem + buf * STAGE + CA + bpos0;
+    bf16x8 fb[2][PL];
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) fb[0][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) {
+#pragma unroll
+        for (int pl = 0; pl < PL; ++pl)
+          fb[(j + 1) & 1][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + (j + 1) * 64);
+      }
+      acc[j] = mfma_planes<PL>(fb[j & 1], fa, acc[j]);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (j + 1 < TN) __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, PL == 3 ? 6 : 1, 0);
+    }
+  };
+  // fused epilogue straight from the Cᵀ accumulators: lane (r, h) of block j holds pixel m0 + 32·wave + r,
+  // channels n0 + 32 j + 8 i + 4 h + {0..3} in acc[j][4i..4i+3]
+  auto epilogue = [&](int ti) {
+    const int wg = t_beg + loc + ti * nloc;
+    const int mt = wg / tilesN;
+    const int n0 = (wg - mt * tilesN) * BN;
+    const int64_t m = (int64_t)mt * BM + wave * 32 + r;
+    if (m < p.M) {
+      const bool vec = p.vec_epi;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float4 r1[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + j * 32 + 8 * i + 4 * h;
+          r1[i] = (vec && d.res1 && n + 3 < d.Cout) ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
+                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + j * 32 + 8 * i + 4 * h;
+          if (n >= d.Cout) continue;
+          const float4 v = make_float4(acc[j][4 * i], acc[j][4 * i + 1], acc[j][4 * i + 2], acc[j][4 * i + 3]);
+          if (vec && n + 3 < d.Cout) epilogue_vec(p, m, n, v, r1[i]);
+          else epilogue_store(p, m, n, v);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[j][q] = 0.f;
+  };
+
+  if (total == 0) return;
+  set_issue_tile(0);
+  // prologue: stream steps 0..2 in flight, step 0 landed, its A planes split
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t)
+    if (t < total) issue(t);
+  if (total >= 3) wait_vmcnt<2 * GLDS>();
+  else if (total == 2) wait_vmcnt<GLDS>();
+  else wait_vmcnt<0>();
+  raw_barrier();
+  split_a(0, fa);
+  const bool first_split = wave < 4;
+  int c_tile = 0, c_k = 0;  // compute cursor
+  for (int t = 0; t < total; ++t) {
+    // stream step t+1 landed (steps up to t+2 issued: one may stay in flight). After an epilogue
+    // interval that wait already happened before the epilogue's stores were issued (below), so the
+    // stores are not waited for here; one interval later they are older than every DMA still
+    // allowed in flight and the plain count covers them.
+    if (!(c_k == 0 && t > 0)) {
+      if (t + 2 < total) wait_vmcnt<GLDS>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();  // everyone is past interval t-1: buffer (t-1) % 4 is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + NS - 1 < total) issue((t + NS - 1) % NS);
+    const bool more = t + 1 < total;
+    if (first_split) {
+      if (more) split_a((t + 1) % NS, fn);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(t % NS);
+    } else {
+      mma(t % NS);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) split_a((t + 1) % NS, fn);
+    }
+#pragma unroll
+    for (int pl = 0; pl < PL; ++pl) fa[pl] = fn[pl];
+    if (++c_k == nk) {
+      // the next interval needs step t+2: wait for it now (steps up to t+3 issued), before the
+      // epilogue's loads and stores enter the count
+      if (t + 3 < total) wait_vmcnt<GLDS>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      epilogue(c_tile);
+      ++c_tile;
+      c_k = 0;
+    }
+  }
+}
+
+template <int TN>
+int launch_x3p(const ConvArgs& a, int planes, hipStream_t s) {
+  if (a.d.Cin % 16 || a.K % 16 || a.splits != 1) {
+    set_error("sp_conv2d: persistent kernel needs Cin %% 16 == 0 and no split-K (Cin=%d)", a.d.Cin);
+    return -1;
+  }
+  constexpr int BN = 32 * TN;
+  const int64_t tiles = ((a.M + 255) / 256) * ((a.d.Cout + BN - 1) / BN);
+  if (tiles > 0x7fffffff) {
+    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+    return -1;
+  }
+  const int grid = (int)(tiles < g_num_cus ? tiles : g_num_cus);
+  if (planes == 3)
+    hipLaunchKernelGGL((conv_x3p_kernel<TN, 3>), dim3(grid), dim3(512), 0, s, a, (int)tiles);
+  else
+    hipLaunchKernelGGL((conv_x3p_kernel<TN, 1>), dim3(grid), dim3(512), 0, s, a, (int)tiles);
+  return check_launch(planes == 3 ? "sp_conv2d(f32x3 persistent)" : "sp_conv2d(bf16 persistent)");
+}
+
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
@@ -1408,6 +1659,13 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 generic)" : "sp_conv2d(bf16 generic)");
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
+  }
+  if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1) {
+    switch (cfg) {
+      case 73: return launch_x3p<8>(a, planes, s);  // 256×256 persistent
+      case 74: return launch_x3p<6>(a, planes, s);  // 256×192 persistent
+      default: return launch_x3p<4>(a, planes, s);  // 256×128 persistent
+    }
   }
   if (cfg >= 70 && cfg <= 72 && !a.d.A2) {
     switch (cfg) {
@@ -1467,7 +1725,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 72 || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 75 || (cfg >= 73 && a.splits > 1) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

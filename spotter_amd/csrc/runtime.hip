@@ -20,6 +20,10 @@ extern "C" int sp_abi_version(void) { return SP_ABI_VERSION; }
 
 extern "C" const char* sp_last_error(void) { return sp::g_err; }
 
+namespace sp {
+int g_num_cus = 256;
+}
+
 extern "C" int sp_device_init(int device) {
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
@@ -37,6 +41,7 @@ extern "C" int sp_device_init(int device) {
                   prop.gcnArchName);
     return -2;
   }
+  sp::g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   return 0;
 }
 
