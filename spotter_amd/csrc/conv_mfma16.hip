@@ -1407,9 +1407,12 @@ __global__ __launch_bounds__(512) void conv_x3p_kernel(const ConvArgs p, int nti
   const int G = gridDim.x;
   const int xcd = blockIdx.x & 7;
   const int loc = blockIdx.x >> 3;
-  const int nloc = (G - xcd + 7) >> 3;
-  const int t_beg = (int)((int64_t)ntiles * xcd / 8);
-  const int t_end = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  const int nloc = (G - xcd + 7) >> 3;  // workgroups with this blockIdx.x % 8
+  int before = 0;                        // workgroups in the groups before this one
+  for (int y = 0; y < xcd; ++y) before += (G - y + 7) >> 3;
+  // group x takes a contiguous tile range in proportion to its workgroups (any grid size)
+  const int t_beg = (int)((int64_t)ntiles * before / G);
+  const int t_end = (int)((int64_t)ntiles * (before + nloc) / G);
   const int my_tiles = t_end - t_beg > loc ? (t_end - t_beg - loc + nloc - 1) / nloc : 0;
   const int nk = p.K / BK;
   const int total = my_tiles * nk;
