@@ -30,6 +30,8 @@
 // share an A row-panel share one L2.
 #include <cstdlib>
 
+#include <type_traits>
+
 #include "conv_common.h"
 
 #ifndef SP_ABLATE
@@ -1523,31 +1525,54 @@ __global__ __launch_bounds__(512) void conv_x3p_kernel(const ConvArgs p, int nti
     }
   };
   // fused epilogue straight from the Cᵀ accumulators: lane (r, h) of block j holds pixel m0 + 32·wave + r,
-  // channels n0 + 32 j + 8 i + 4 h + {0..3} in acc[j][4i..4i+3]
+  // channels n0 + 32 j + 8 i + 4 h + {0..3} in acc[j][4i..4i+3]. The activation is a template argument
+  // (one straight-line copy per activation) so the unrolled body stays small enough for acc[] to
+  // remain in registers.
+  auto epi_body = [&](auto act_tag, int64_t m, int n0) {
+    constexpr int ACT = decltype(act_tag)::value;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      float4 r1[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + j * 32 + 8 * i + 4 * h;
+        r1[i] = (d.res1 && n < d.Cout) ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
+                                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + j * 32 + 8 * i + 4 * h;
+        float4 v = make_float4(acc[j][4 * i], acc[j][4 * i + 1], acc[j][4 * i + 2], acc[j][4 * i + 3]);
+        if (n < d.Cout) {
+          if (d.row_scale) {
+            const float rs = d.row_scale[m % d.row_period];
+            v.x *= rs; v.y *= rs; v.z *= rs; v.w *= rs;
+          }
+          const float4 sc = d.scale ? *reinterpret_cast<const float4*>(d.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+          const float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+          v.x = fmaf(v.x, sc.x, sh.x) + r1[i].x; v.y = fmaf(v.y, sc.y, sh.y) + r1[i].y;
+          v.z = fmaf(v.z, sc.z, sh.z) + r1[i].z; v.w = fmaf(v.w, sc.w, sh.w) + r1[i].w;
+          v.x = act_apply(v.x, ACT); v.y = act_apply(v.y, ACT); v.z = act_apply(v.z, ACT); v.w = act_apply(v.w, ACT);
+          if (d.res2) {
+            const float4 a2 = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
+            v.x += a2.x; v.y += a2.y; v.z += a2.z; v.w += a2.w;
+          }
+          *reinterpret_cast<float4*>(out_row(d, m) + n) = v;
+        }
+      }
+    }
+  };
   auto epilogue = [&](int ti) {
     const int wg = t_beg + loc + ti * nloc;
     const int mt = wg / tilesN;
     const int n0 = (wg - mt * tilesN) * BN;
     const int64_t m = (int64_t)mt * BM + wave * 32 + r;
     if (m < p.M) {
-      const bool vec = p.vec_epi;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        float4 r1[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + j * 32 + 8 * i + 4 * h;
-          r1[i] = (vec && d.res1 && n + 3 < d.Cout) ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
-                                                     : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + j * 32 + 8 * i + 4 * h;
-          if (n >= d.Cout) continue;
-          const float4 v = make_float4(acc[j][4 * i], acc[j][4 * i + 1], acc[j][4 * i + 2], acc[j][4 * i + 3]);
-          if (vec && n + 3 < d.Cout) epilogue_vec(p, m, n, v, r1[i]);
-          else epilogue_store(p, m, n, v);
-        }
+      switch (d.act) {
+        case SP_ACT_RELU: epi_body(std::integral_constant<int, SP_ACT_RELU>{}, m, n0); break;
+        case SP_ACT_SILU: epi_body(std::integral_constant<int, SP_ACT_SILU>{}, m, n0); break;
+        case SP_ACT_GELU: epi_body(std::integral_constant<int, SP_ACT_GELU>{}, m, n0); break;
+        default: epi_body(std::integral_constant<int, SP_ACT_NONE>{}, m, n0); break;
       }
     }
 #pragma unroll
@@ -1609,8 +1634,9 @@ __global__ __launch_bounds__(512) void conv_x3p_kernel(const ConvArgs p, int nti
 
 template <int TN>
 int launch_x3p(const ConvArgs& a, int planes, hipStream_t s) {
-  if (a.d.Cin % 16 || a.K % 16 || a.splits != 1) {
-    set_error("sp_conv2d: persistent kernel needs Cin %% 16 == 0 and no split-K (Cin=%d)", a.d.Cin);
+  if (a.d.Cin % 16 || a.K % 16 || a.splits != 1 || !a.vec_epi) {
+    set_error("sp_conv2d: persistent kernel needs Cin %% 16 == 0, no split-K and 16-byte aligned C / residual "
+              "/ BN rows with Cout %% 4 == 0 (Cin=%d Cout=%d)", a.d.Cin, a.d.Cout);
     return -1;
   }
   constexpr int BN = 32 * TN;
@@ -1663,7 +1689,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
-  if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1) {
+  if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1 && a.vec_epi) {
     switch (cfg) {
       case 73: return launch_x3p<8>(a, planes, s);  // 256×256 persistent
       case 74: return launch_x3p<6>(a, planes, s);  // 256×192 persistent
@@ -1728,7 +1754,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
     }
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 75 || (cfg >= 73 && a.splits > 1) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 75 || (cfg >= 73 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes
