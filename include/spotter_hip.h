@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 7
+#define SP_ABI_VERSION 8
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -88,6 +88,14 @@ typedef struct {
   int32_t precision;         /* sp_precision */
   const uint16_t* Wt_bf16;   /* [Cout][K] bf16 weights (SP_PREC_BF16), [3][Cout][K] (SP_PREC_F32X3) */
   int64_t wt_plane_stride;   /* elements between the hi / mid / lo planes (SP_PREC_F32X3) */
+  /* Optional row LayerNorm fused into the epilogue (ABI v8): when ln_gamma is set,
+   *   out[m, :] = LayerNorm(acc·row_scale·scale + shift + res1)[m, :] · ln_gamma + ln_beta   (eps ln_eps)
+   * over the whole output row — the post-norm "Linear → +residual → LayerNorm" of the AIFI and decoder
+   * layers (M2:395-404, 409-423, 426-429, 856-904) and enc_output (M2:1376-1381). Needs the fp32 weights
+   * (precision SP_PREC_FP32), Cout a multiple of 128 up to 512, act none, no res2 / grouped rows. */
+  const float* ln_gamma;
+  const float* ln_beta;
+  float ln_eps;
 } sp_conv_desc;
 
 /*

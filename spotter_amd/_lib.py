@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -41,6 +41,7 @@ class SpConvDesc(C.Structure):
         ("out_rows_per_group", i32), ("out_group_stride", i64),
         ("workspace", vp), ("workspace_elems", i64),
         ("precision", i32), ("Wt_bf16", vp), ("wt_plane_stride", i64),
+        ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
     ]
 
 

@@ -184,6 +184,61 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
   }
 }
 
+// Row-LayerNorm epilogue (sp_conv_desc.ln_gamma): the workgroup holds whole output rows — BM = 32 rows
+// × BN = Cout columns, 4 waves side by side along N, each wave's 32 × 32·TN accumulators (v_mfma_f32_32x32x*
+// layout) — staged in LDS, then one wave per row: bias / BN affine, residual, two-pass mean and variance
+// over the row (the sp_layernorm arithmetic), gamma / beta, 4-byte-per-lane coalesced stores.
+template <int TN>
+__device__ __forceinline__ void epilogue_rowln(const ConvArgs& p, float* tile, const f32x16* acc, int64_t m0,
+                                               int wave, int lane) {
+  constexpr int BN = 128 * TN;
+  constexpr int LDT = BN + 4;
+  constexpr int PER = BN / 64;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tile[((q & 3) + 8 * (q >> 2) + 4 * h) * LDT + wave * 32 * TN + j * 32 + r] = acc[j][q];
+  __syncthreads();
+  const sp_conv_desc& d = p.d;
+  const int N = d.Cout;
+  for (int rr = wave; rr < 32; rr += 4) {
+    const int64_t m = m0 + rr;
+    if (m >= p.M) break;
+    const float rs = d.row_scale ? d.row_scale[m % d.row_period] : 1.0f;
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = lane + 64 * u;
+      float x = 0.f;
+      if (c < N) {
+        x = fmaf(tile[rr * LDT + c] * rs, d.scale ? d.scale[c] : 1.0f, d.shift ? d.shift[c] : 0.0f);
+        if (d.res1) x += d.res1[m * d.ldr1 + c];
+      }
+      v[u] = x;
+      s += x;
+    }
+    const float mean = wave_sum(s) / (float)N;
+    float q = 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = lane + 64 * u;
+      const float t = c < N ? v[u] - mean : 0.f;
+      q += t * t;
+    }
+    const float var = wave_sum(q) / (float)N;
+    const float rstd = 1.0f / sqrtf(var + d.ln_eps);
+    float* orow = out_row(d, m);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int c = lane + 64 * u;
+      if (c < N) orow[c] = (v[u] - mean) * rstd * d.ln_gamma[c] + d.ln_beta[c];
+    }
+  }
+}
+
 // conv_mfma16.hip: bf16-operand MFMA GEMM (planes = 1: bf16; planes = 3: fp32 via a 3-way bf16
 // split). cfg < 0 picks the tile by shape. Returns 0 or the launch error.
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s);

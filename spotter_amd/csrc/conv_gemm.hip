@@ -40,7 +40,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 
 // WM × WN waves (WM·WN = 4), each a (32·TM) × (32·TN) patch: 2×2 is the square default, 4×1 gives
 // the 32- and 64-wide N tiles that thin outputs (Cout = 32 / 64: stem, stage 1) need without idle MFMAs.
-template <int TM, int TN, int DB, int WM = 2>
+template <int TM, int TN, int DB, int WM = 2, bool LN = false>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   constexpr int WN = 4 / WM;
   static_assert(WM * WN == 4, "four waves per workgroup");
@@ -49,7 +49,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   constexpr int PA = BM / 32;  // loader passes (32 rows per pass)
   constexpr int PB = BN / 32;
   constexpr int STAGE = (BM + BN) * BK;
-  constexpr int EPI = 4 * 32 * (TN * 32);  // epilogue: one 32×(32·TN) slab per wave
+  constexpr int EPI = LN ? 32 * (BN + 4) : 4 * 32 * (TN * 32);  // epilogue: one 32×(32·TN) slab per wave,
+                                                                 // or the 32 whole rows of a LayerNorm tile
   constexpr int SMEM = STAGE * (DB ? 2 : 1) > EPI ? STAGE * (DB ? 2 : 1) : EPI;
   __shared__ __attribute__((aligned(16))) float smem[SMEM];
 
@@ -228,6 +229,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   // of one output row (16-byte loads of res1/res2/scale/shift, 16-byte stores):
   // pass i moves each wave's 32-row band acc[i][*] to its private LDS slab.
   __syncthreads();  // main loop done with the operand stages
+  if constexpr (LN) {
+    static_assert(WM == 1 && TM == 1, "row LayerNorm tiles are 32 rows × the whole N");
+    epilogue_rowln<TN>(p, smem, acc[0], m0, wave, lane);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
     epilogue_band<TN>(p, smem + wave * (32 * TN * 32), acc[i], m0 + wm * TM * 32 + i * 32,
@@ -250,11 +256,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
   }
 }
 
-template <int TM, int TN, int DB, int WM = 2>
+template <int TM, int TN, int DB, int WM = 2, bool LN = false>
 int launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * (4 / WM) * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM), a.splits);
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM>), grid, dim3(256), 0, s, a);
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, a);
   int rc = check_launch("sp_conv2d");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -350,6 +356,19 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     }
   }
   hipStream_t s = as_stream(stream);
+  if (d->ln_gamma) {  // Linear → +residual → LayerNorm in one launch: 32-row tiles holding whole rows
+    SP_ARG_CHECK(planes == 0 && d->Cout % 128 == 0 && d->Cout <= 512 && d->act == SP_ACT_NONE && !d->res2 &&
+                     d->out_rows_per_group == 0 && d->ln_beta && a.fast,
+                 "sp_conv2d: fused LayerNorm needs fp32 weights, Cout %% 128 == 0 <= 512, no act / res2 / "
+                 "grouped rows, Cin %% 32 == 0 (Cout=%d)", d->Cout);
+    a.splits = 1;
+    switch (d->Cout / 128) {
+      case 1: return launch<1, 1, 1, 1, true>(a, s);
+      case 2: return launch<1, 2, 1, 1, true>(a, s);
+      case 3: return launch<1, 3, 1, 1, true>(a, s);
+      default: return launch<1, 4, 1, 1, true>(a, s);
+    }
+  }
   // tile choice: a test / tuning override, else the measured exact-shape table (tile_table.h),
   // else the by-shape rules below and in launch_mfma16
   int cfg = forced_cfg();

@@ -133,7 +133,8 @@ class Engine:
     """Owns the packed device weights and the per-shape workspaces of one GPU."""
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
-                 fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True):
+                 fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
+                 fuse_ln: bool = True):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -141,6 +142,7 @@ class Engine:
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
         self.fuse_shortcut = fuse_shortcut  # bottleneck tail + projection shortcut as one GEMM (_fused_tail)
+        self.fuse_ln = fuse_ln  # post-norm LayerNorms in the preceding GEMM's epilogue (_lin_op ln=)
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
@@ -358,7 +360,18 @@ class Engine:
                           shift=cw.shift, act=act, res1=res1, res2=res2,
                           workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)
 
-    def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None):
+    def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None,
+                ln=None):
+        """ln = (gamma, beta): the post-norm LayerNorm of the output row fused into the GEMM epilogue
+        (fp32-MFMA tile holding whole rows; sp_conv_desc.ln_gamma)."""
+        if ln is not None and self.fuse_ln:
+            return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, res1=res1, a2=a2, row_scale=row_scale,
+                              ln=(ln[0], ln[1], self.cfg.layer_norm_eps))
+        if ln is not None:  # unfused: GEMM into a scratch row block, then sp_layernorm into `out`
+            tmp = view(self._buf("ln_tmp", rows, lw.n), lw.n)
+            ops.linear(x, rows, lw.k, lw.w, lw.n, tmp, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
+                       row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
+            return ops.layernorm(tmp, *ln, out, rows, lw.n, self.cfg.layer_norm_eps)
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                           row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
@@ -498,10 +511,8 @@ class Engine:
         qk = self._buf("aifi_qk", rows, 2 * Hd)
         vv = self._buf("aifi_v", rows, Hd)
         at = self._buf("aifi_at", rows, Hd)
-        t1 = self._buf("aifi_t1", rows, Hd)
         y1 = self._buf("aifi_y1", rows, Hd)
         ff = self._buf("aifi_ff", rows, cfg.encoder_ffn_dim)
-        t2 = self._buf("aifi_t2", rows, Hd)
         p5a = self._buf("p5a", rows, Hd)
         # with config.eval_size set HF runs AIFI without the position embedding (M2:1073-1081)
         self._lin_op(view(p5, Hd), rows, A["qk"], view(qk, 2 * Hd), a2=None if cfg.eval_size else view(pos, Hd))
@@ -509,11 +520,9 @@ class Engine:
         heads = cfg.encoder_attention_heads
         ops.attention(V(qk, 0, 2 * Hd), V(qk, Hd, 2 * Hd), view(vv, Hd), view(at, Hd), B, n, heads, Hd // heads,
                       (Hd // heads) ** -0.5)
-        self._lin_op(view(at, Hd), rows, A["o"], view(t1, Hd), res1=view(p5, Hd))
-        ops.layernorm(view(t1, Hd), *A["ln1"], view(y1, Hd), rows, Hd, cfg.layer_norm_eps)
+        self._lin_op(view(at, Hd), rows, A["o"], view(y1, Hd), res1=view(p5, Hd), ln=A["ln1"])
         self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act=self.act_aifi)
-        self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(t2, Hd), res1=view(y1, Hd))
-        ops.layernorm(view(t2, Hd), *A["ln2"], view(p5a, Hd), rows, Hd, cfg.layer_norm_eps)
+        self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(p5a, Hd), res1=view(y1, Hd), ln=A["ln2"])
         yield
         # FPN (M2:1183-1197)
         self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act=self.act_enc)
@@ -653,11 +662,9 @@ class Engine:
         anchors, valid = self._const(("anchors", tuple(shapes)), lambda: tuple(
             _t(a, self.dev) for a in anchors_for(shapes)))
         rows = B * S
-        om_pre = self._buf("om_pre", rows, D)
         om = self._buf("om", rows, D)
         cls = self._buf("enc_cls", rows, NC)
-        self._lin_op(view(src, D), rows, self.enc_output, view(om_pre, D), row_scale=valid)
-        ops.layernorm(view(om_pre, D), *self.enc_ln, view(om, D), rows, D, cfg.layer_norm_eps)
+        self._lin_op(view(src, D), rows, self.enc_output, view(om, D), row_scale=valid, ln=self.enc_ln)
         self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
         topk = self._buf("topk", B, Q, dtype=torch.int32)
         cmax = self._buf("enc_cls_max", rows)
@@ -685,7 +692,6 @@ class Engine:
         qk = self._buf("dec_qk", Bq, 2 * D)
         vv = self._buf("dec_v", Bq, D)
         at = self._buf("dec_at", Bq, D)
-        tmp = self._buf("dec_tmp", Bq, D)
         offaw = self._buf("dec_offaw", Bq, nH * nL * nP * 3)
         ff = self._buf("dec_ff", Bq, cfg.decoder_ffn_dim)
         for j, P in enumerate(self.dec):
@@ -696,18 +702,15 @@ class Engine:
             self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
             ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
                           (D // nH) ** -0.5)
-            self._lin_op(view(at, D), Bq, P["o"], view(tmp, D), res1=view(h, D))
-            ops.layernorm(view(tmp, D), *P["ln1"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            self._lin_op(view(at, D), Bq, P["o"], view(h, D), res1=view(h, D), ln=P["ln1"])  # in place: row-local
             # deformable cross-attention (M2:409-423)
             self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
             ops.msda(V(vall, 0, L * D), j * D, view(offaw, nH * nL * nP * 3), ref, view(at, D), B, S, Q, nH,
                      D // nH, shapes, starts, nP, cfg.decoder_offset_scale)
-            self._lin_op(view(at, D), Bq, P["out"], view(tmp, D), res1=view(h, D))
-            ops.layernorm(view(tmp, D), *P["ln2"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            self._lin_op(view(at, D), Bq, P["out"], view(h, D), res1=view(h, D), ln=P["ln2"])
             # FFN (M2:426-429)
             self._lin_op(view(h, D), Bq, P["fc1"], view(ff, cfg.decoder_ffn_dim), act=self.act_dec)
-            self._lin_op(view(ff, cfg.decoder_ffn_dim), Bq, P["fc2"], view(tmp, D), res1=view(h, D))
-            ops.layernorm(view(tmp, D), *P["ln3"], view(h, D), Bq, D, cfg.layer_norm_eps)
+            self._lin_op(view(ff, cfg.decoder_ffn_dim), Bq, P["fc2"], view(h, D), res1=view(h, D), ln=P["ln3"])
             # iterative box refinement (M2:636-639)
             b0, b1, b2 = P["bbox"]
             self._lin_op(view(h, D), Bq, b0, view(t_a, D), act="relu")

@@ -71,8 +71,9 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
-           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None):
-    """wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
+           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None):
+    """ln = (gamma, beta, eps): LayerNorm over each output row fused into the epilogue (fp32 weights).
+    wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
     wt_planes (int16 [3, Cout*K]: the hi / mid / lo bf16 split of the fp32 weights, split_bf16x3)
     selects the fp32-accurate 3-way-split path (SP_PREC_F32X3)."""
     ho = (h + 2 * pad - k) // stride + 1
@@ -131,6 +132,13 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         d.precision = 2
         d.Wt_bf16 = wt_planes.data_ptr()
         d.wt_plane_stride = wt_planes.shape[1]
+    if ln is not None:
+        g, b, eps = ln
+        if wt16 is not None or wt_planes is not None:
+            raise ValueError("conv: the fused LayerNorm runs on the fp32 weights")
+        if g.numel() < cout or b.numel() < cout:
+            raise ValueError("conv: LayerNorm gamma / beta shorter than Cout")
+        d.ln_gamma, d.ln_beta, d.ln_eps = g.data_ptr(), b.data_ptr(), float(eps)
     if workspace is not None:
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
@@ -138,15 +146,16 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     nbytes = 4 * (n * h * w * cin * (2 if a2 is not None else 1) + cout * k * k * cin + m * cout
                   * (1 + (res1 is not None) + (res2 is not None)))
     _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
-            (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision]))
+            (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision] if ln is None else "f32+ln"))
     return ho, wo
 
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
            res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
-           scale=None, workspace=None, wt16=None, wt_planes=None):
+           scale=None, workspace=None, wt16=None, wt_planes=None, ln=None):
     return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
-                  res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes)
+                  res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes,
+                  ln=ln)
 
 
 def bf16_bits(a) -> np.ndarray:

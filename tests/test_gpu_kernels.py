@@ -523,3 +523,28 @@ def test_rowmax(dev, rows, c, ld):
     out = torch.empty(rows, device=dev)
     ops.rowmax(view(T(x.reshape(-1), dev), ld), rows, c, out)
     np.testing.assert_array_equal(out.cpu().numpy(), x[:, :c].max(1))
+
+
+@pytest.mark.parametrize("rows,k,n", [(1, 256, 256), (37, 1024, 256), (9600, 256, 256), (130, 384, 384),
+                                      (64, 2048, 384), (33, 256, 512)])
+def test_linear_fused_layernorm(dev, rows, k, n):
+    """sp_conv2d with ln_gamma: Linear (+ row mask, bias, residual) → LayerNorm over the row in one launch
+    (the AIFI / decoder post-norm and enc_output, M2:395-429, 856-904, 1376-1381), vs fp64."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    rng = np.random.default_rng(rows * 7 + n)
+    x = rng.standard_normal((rows, k)).astype(np.float32)
+    w = (rng.standard_normal((n, k)) / np.sqrt(k)).astype(np.float32)
+    b = rng.standard_normal(n).astype(np.float32) * 0.1
+    res = rng.standard_normal((rows, n)).astype(np.float32)
+    rs = (rng.uniform(0, 1, 11) > 0.3).astype(np.float32)
+    g = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    be = rng.standard_normal(n).astype(np.float32) * 0.1
+    t = (x.astype(np.float64) @ w.T.astype(np.float64)) * rs[np.arange(rows) % 11, None] + b + res
+    mu = t.mean(1, keepdims=True)
+    ref = (t - mu) / np.sqrt(((t - mu) ** 2).mean(1, keepdims=True) + 1e-5) * g + be
+    out = torch.zeros(rows * n, device=dev)
+    ops.linear(view(T(x.reshape(-1), dev), k), rows, k, T(w, dev), n, view(out, n), bias=T(b, dev),
+               res1=view(T(res.reshape(-1), dev), n), row_scale=T(rs, dev), ln=(T(g, dev), T(be, dev), 1e-5))
+    np.testing.assert_allclose(out.cpu().numpy().reshape(rows, n), ref, rtol=1e-4, atol=1e-4)

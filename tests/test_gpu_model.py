@@ -298,3 +298,24 @@ def test_request_microbatching_matches_single_calls():
     assert b.images == 13 and b.batches < 13, (b.batches, b.images)
     for i in range(12):
         np.testing.assert_allclose(np.sort(got[i].max(-1)), np.sort(ref[i].max(-1)), rtol=0, atol=SCORE_TOL)
+
+
+@pytest.mark.parametrize("preset", ["r18vd", "r101vd"])
+def test_fused_layernorm_matches_unfused(preset):
+    """The post-norm LayerNorms fused into the preceding GEMM epilogues (Engine fuse_ln) against the
+    separate GEMM + sp_layernorm path: fp32 reassociation only, so at the parity bar."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+    from spotter_amd.synthetic import synthetic_image
+
+    cfg = PRESETS[preset]
+    w = SpotterForObjectDetection(cfg)._host_weights()
+    x = SpotterImageProcessor()(images=[synthetic_image(21), synthetic_image(22)])["pixel_values"].cuda()
+    res = []
+    for fuse in (True, False):
+        eng = Engine(cfg, w, "cuda", fuse_ln=fuse)
+        lg, bx = eng.forward(x)
+        res.append(np.sort(torch.sigmoid(lg).cpu().numpy().max(-1), axis=-1))
+    # queries compared as sorted per-query scores: a near-tie in the top-300 may swap query order
+    np.testing.assert_allclose(res[0], res[1], rtol=0, atol=SCORE_TOL)
