@@ -134,7 +134,7 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = True):
+                 fuse_ln: bool = False):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -142,7 +142,11 @@ class Engine:
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
         self.fuse_shortcut = fuse_shortcut  # bottleneck tail + projection shortcut as one GEMM (_fused_tail)
-        self.fuse_ln = fuse_ln  # post-norm LayerNorms in the preceding GEMM's epilogue (_lin_op ln=)
+        # post-norm LayerNorms in the preceding GEMM's epilogue (_lin_op ln=). Off by default: the fused
+        # kernel needs whole rows per workgroup (32-row fp32-MFMA tiles), which at bs32 ran the 21 GEMMs at
+        # 42 TF/s (2.47 ms/step) against 1.4 ms/step for the unfused GEMMs + 21 sp_layernorm launches
+        # (profiles/r2/fused_ln_ab.json); it stays selectable and tested.
+        self.fuse_ln = fuse_ln
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
