@@ -372,7 +372,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   // tile choice: a test / tuning override, else the measured exact-shape table (tile_table.h),
   // else the by-shape rules below and in launch_mfma16
   int cfg = forced_cfg();
-  if (cfg < 0 && a.splits == 1 && planes != 1)
+  if (cfg < 0 && a.splits == 1)
     cfg = tile_table_lookup(a.M, d->Cout, a.K, d->KH, d->stride, planes);
   if (planes) return launch_mfma16(a, planes, cfg, s);
   if (a.splits > 1) return launch<1, 1, 0>(a, s);

@@ -47,7 +47,12 @@ def time_one(dev, m, cout, K, k, stride, mode, cfg, reps):
     x = torch.randn(n * h * w * cin, device=dev, generator=g)
     wt = torch.randn(cout * K, device=dev, generator=g) * (1.0 / K ** 0.5)
     out = torch.empty(m * cout, device=dev)
-    kw = {"wt_planes": ops.split_bf16x3(wt)} if mode == "x3" else {}
+    if mode == "x3":
+        kw = {"wt_planes": ops.split_bf16x3(wt)}
+    elif mode == "bf16":
+        kw = {"wt16": torch.from_numpy(ops.bf16_bits(wt.cpu().numpy()).view("int16")).to(dev)}
+    else:
+        kw = {}
     ops.force_conv_config(None if cfg == "-" else cfg)
 
     def run():
@@ -84,11 +89,11 @@ def main():
     for r in rows:
         m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])
         per_step = r["ms"] / a.steps
-        if mode not in ("x3", "f32") or per_step < a.min_ms:
+        if mode not in ("x3", "f32", "bf16") or per_step < a.min_ms:
             continue
         launches = r["launches"] / a.steps
         times = {}
-        for cfg in (X3_CFGS if mode == "x3" else F32_CFGS):
+        for cfg in (F32_CFGS if mode == "f32" else X3_CFGS):
             t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps)
             if t is not None:
                 times[cfg] = round(t, 4)
