@@ -385,6 +385,11 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     case 121: return launch<1, 2, 1>(a, s);
     case 110: return launch<1, 1, 0>(a, s);
     case 111: return launch<1, 1, 1>(a, s);
+    // 1×4 wave grids: "1<TM><TN><DB>" → tile 32 × (128·TN) (small-M linears: more workgroups)
+    case 1110: return launch<1, 1, 0, 1>(a, s);
+    case 1111: return launch<1, 1, 1, 1>(a, s);
+    case 1120: return launch<1, 2, 0, 1>(a, s);
+    case 1121: return launch<1, 2, 1, 1>(a, s);
     // 4×1 wave grids: "4<TM><TN><DB>" → tile (128·TM) × (32·TN)
     case 4110: return launch<1, 1, 0, 4>(a, s);
     case 4111: return launch<1, 1, 1, 4>(a, s);

@@ -99,7 +99,8 @@ def test_conv2d_matches_oracle(dev, case, workspace=None):
 
 
 @pytest.mark.parametrize("cfg", ["220", "221", "210", "211", "120", "121", "110", "111",
-                                 "4110", "4111", "4210", "4211", "4120", "4121"])
+                                 "4110", "4111", "4210", "4211", "4120", "4121",
+                                 "1110", "1111", "1120", "1121"])
 def test_conv2d_every_tile_config(dev, cfg, monkeypatch):
     """Each tile variant (sp_set_conv_config override) on a ragged 3×3 and a 1×1 with residuals."""
     from spotter_amd import ops

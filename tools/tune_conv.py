@@ -24,7 +24,8 @@ from spotter_amd.ops import view
 
 X3_CFGS = ["-", "11", "12", "13", "14", "16", "17", "33", "41", "44", "45", "46", "50", "51", "62", "63", "64",
            "70", "71", "72"]
-F32_CFGS = ["-", "110", "111", "120", "121", "210", "211", "220", "221", "4110", "4111", "4210", "4120"]
+F32_CFGS = ["-", "110", "111", "120", "121", "210", "211", "220", "221", "4110", "4111", "4210", "4120", "1110", "1111",
+            "1120", "1121"]
 
 
 def geometry(m, cout, K, k, stride):
@@ -82,6 +83,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--min-ms", type=float, default=0.05, help="skip shapes cheaper than this per step")
     ap.add_argument("--steps", type=int, default=10, help="steps the detail file was recorded over")
+    ap.add_argument("--modes", default="x3,f32,bf16", help="operand modes to tune")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rows = json.load(open(a.detail))
@@ -89,7 +91,7 @@ def main():
     for r in rows:
         m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])
         per_step = r["ms"] / a.steps
-        if mode not in ("x3", "f32", "bf16") or per_step < a.min_ms:
+        if mode not in a.modes.split(",") or per_step < a.min_ms:
             continue
         launches = r["launches"] / a.steps
         times = {}
