@@ -143,8 +143,12 @@ class KernelEventRecorder:
     def classes(self):
         """kind -> dict(ms = sum of launch durations, busy = union of launch intervals, flops, bytes, n)."""
         out = {}
-        for k, e0, e1, f, nb, _ in self.recs:
-            c = out.setdefault(k, {"ms": 0.0, "ivs": [], "flops": 0, "bytes": 0, "n": 0})
+        for k, e0, e1, f, nb, shp in self.recs:
+            c = out.setdefault(k, {"ms": 0.0, "ivs": [], "flops": 0, "bytes": 0, "n": 0, "gather": 0})
+            if k == "msda" and shp:
+                # bytes the bilinear taps fetch (4 corners × Dh fp32 per sample), L2-served: SURVEY §8 D1.4
+                B_, S_, Q_, H_, Dh_, L_, P_ = shp
+                c["gather"] += B_ * Q_ * H_ * L_ * P_ * 4 * Dh_ * 4
             a, b = self.t0.elapsed_time(e0), self.t0.elapsed_time(e1)
             c["ms"] += b - a
             c["ivs"].append((a, b))
@@ -445,6 +449,12 @@ def main():
             classes[kind] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                              "frac": round(ach / peak, 4), "ms_per_step": round(c["busy"] / args.steps, 3),
                              "launches_per_step": c["n"] // args.steps}
+            if c.get("gather"):
+                classes[kind]["l2_gather"] = {
+                    "achieved": round(c["gather"] / 1e9 / (c["busy"] * 1e-3), 1), "unit": "GB/s",
+                    "bytes_per_launch": c["gather"] // c["n"],
+                    "note": "sampled-corner bytes (4 taps × Dh × 4 B per sample); the value map stays in L2 / "
+                            "Infinity Cache, so the compulsory-bytes figure above is not an HBM bound"}
         roof = conv_roofline(rec, cl, args, bf)
 
     if rec is not None and args.detail and rank == 0:

@@ -496,6 +496,22 @@ def test_preprocess_bit_exact(dev, out):
         np.testing.assert_array_equal(got[i], preprocess(im, (out, out)), err_msg=str(PRE_SIZES[i]))
 
 
+@pytest.mark.parametrize("out", [640, 1280, 36])
+def test_preprocess_same_size_fast_path(dev, out):
+    """A batch whose sources all have the output size takes the rescale + CHW kernel (Pillow returns the
+    image unchanged there); bit-exact with the oracle like the resampling path."""
+    from oracle.pil_resize import preprocess
+    from spotter_amd import ops
+    from spotter_amd.synthetic import synthetic_image
+
+    imgs = [synthetic_image(900 + i, out, out) for i in range(3)]
+    res = torch.empty(len(imgs) * 3 * out * out, device=dev)
+    ops.preprocess_u8([T(im, dev) for im in imgs], res, out, out)
+    got = res.cpu().numpy().reshape(len(imgs), 3, out, out)
+    for i, im in enumerate(imgs):
+        np.testing.assert_array_equal(got[i], preprocess(im, (out, out)))
+
+
 def test_preprocess_matches_golden_digests(dev):
     """sha256 of the HF processor's pixel_values (tests/golden/preprocess.npz) — incl. test_pic.jpg."""
     from PIL import Image
