@@ -42,6 +42,12 @@
 #ifndef SP_X3S_ABL
 #define SP_X3S_ABL 0
 #endif
+// Diagnostic build only (-DSP_X3S_STAMP): s_memtime stamps of the first 64 intervals of every wave of
+// workgroup 0 of a conv_x3s_kernel launch, stored by lane 0 with vector stores, read back with
+// sp_debug_x3s_stamps (tools/microbench/x3s_stamps.py). Not in the product build.
+#ifndef SP_X3S_STAMP
+#define SP_X3S_STAMP 0
+#endif
 
 namespace sp {
 
@@ -350,6 +356,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
 // the fp32 kernel's swizzle), position q of a B row holds chunk q ^ ((r >> 2) & 3) (sw16).
 // Padding taps, rows past M and columns past Cout read a 128-byte zero block instead.
 __device__ float4 g_zero_chunk[8];
+#if SP_X3S_STAMP
+__device__ unsigned long long g_x3s_stamps[8 * 64 * 8];
+#endif
 
 template <int PL>
 __device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, bf16x8* out) {
@@ -1183,21 +1192,23 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
   }
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-  auto issue = [&](int kt, int buf) {
-    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+  // DMA of one k-step in two halves: issue_prep computes the GLDS source addresses (and advances the
+  // tap walk), issue_piece(i) issues piece i — the pieces go out one per MFMA block inside mma(), so
+  // their issue cost lands in MFMA gaps instead of a DMA burst after the barrier.
+  const void* isrc[GLDS];
+  uint32_t ist = 0;
+  auto issue_prep = [&](int kt, int buf) {
+    ist = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
     const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
       const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
-      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
-      glds16(src, st + j * NT * 16);
+      isrc[j] = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
     }
     const int k0 = kt * BK;
 #pragma unroll
-    for (int pl = 0; pl < PL; ++pl) {
-      const void* src = b_ok ? static_cast<const void*>(b_ptr + pl * wps + k0) : static_cast<const void*>(zero + cbk * 16);
-      glds16(src, st + (CA + pl * CB) * 16);
-    }
+    for (int pl = 0; pl < PL; ++pl)
+      isrc[GA + pl] = b_ok ? static_cast<const void*>(b_ptr + pl * wps + k0) : static_cast<const void*>(zero + cbk * 16);
     s_c0 += BK;
     if (s_c0 >= d.Cin) {
       s_c0 = 0;
@@ -1206,6 +1217,14 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
         ++s_kh;
       }
     }
+  };
+  auto issue_piece = [&](int i) {
+    glds16(isrc[i], ist + (i < GA ? i * NT * 16 : (CA + (i - GA) * CB) * 16));
+  };
+  auto issue = [&](int kt, int buf) {
+    issue_prep(kt, buf);
+#pragma unroll
+    for (int i = 0; i < GLDS; ++i) issue_piece(i);
   };
 
   const int r = lane & 31;
@@ -1237,7 +1256,10 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
   // B fragments double-buffered in registers: block j+1's ds_reads are issued before block j's
   // MFMAs, so each wait covers loads issued one 6-MFMA group (192 cycles) earlier.
   const int bpos0 = r * 2 + (h ^ ((r >> 3) & 1));  // (brow >> 3) & 1 is the same for brow = j·32 + r
-  auto mma = [&](int buf) {
+  // per block j: the ds_reads of block j+1, then j's MFMAs, then (when this interval issues DMA) DMA
+  // piece j — fenced in that order, so each wait covers loads issued one MFMA group earlier and each
+  // DMA piece's issue cost sits between MFMAs
+  auto mma = [&](int buf, bool dma) {
     const uint4* st = smem + buf * STAGE + CA + bpos0;
     bf16x8 fb[2][PL];
 #pragma unroll
@@ -1249,19 +1271,19 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
         for (int pl = 0; pl < PL; ++pl)
           fb[(j + 1) & 1][pl] = *reinterpret_cast<const bf16x8*>(st + pl * CB + (j + 1) * 64);
       }
+      __builtin_amdgcn_sched_barrier(0);
 #if SP_X3S_ABL & 4
       for (int pl = 0; pl < PL; ++pl) asm volatile("" ::"v"(fa[pl]), "v"(fb[j & 1][pl]));
 #else
       acc[j] = mfma_planes<PL>(fa, fb[j & 1], acc[j]);
 #endif
+      __builtin_amdgcn_sched_barrier(0);
+      if (j < GLDS && dma) issue_piece(j);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // issue order: block 0's ds_reads; then per block j the ds_reads of block j+1 ahead of j's MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (j + 1 < TN) __builtin_amdgcn_sched_group_barrier(0x100, PL, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, PL == 3 ? 6 : 1, 0);
-    }
+    for (int i = TN; i < GLDS; ++i)
+      if (dma) issue_piece(i);
   };
 
   // prologue: steps 0..2 in flight, step 0 landed, its A planes split
@@ -1276,27 +1298,51 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
     split_a(0, fa);
   }
   const bool first_split = wave < 4;
+#if SP_X3S_STAMP
+  const bool stamp_wg = blockIdx.x == 0 && blockIdx.z == 0 && lane == 0;
+#define X3S_STAMP(k)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    if (stamp_wg && t < 64) g_x3s_stamps[(wave * 64 + t) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+#else
+#define X3S_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
   for (int t = 0; t < nk; ++t) {
+    X3S_STAMP(0);
     // step t+1 landed (steps up to t+2 issued: one step may stay in flight)
     if (t + 2 < nk) wait_vmcnt<GLDS>();
     else wait_vmcnt<0>();
+    X3S_STAMP(1);
     __builtin_amdgcn_sched_barrier(0);
 #if !(SP_X3S_ABL & 8)
     raw_barrier();  // everyone is past interval t-1: buffer (t-1) % 4 is free
 #endif
     __builtin_amdgcn_sched_barrier(0);
+    X3S_STAMP(2);
 #if !(SP_X3S_ABL & 1)
-    if (t + NS - 1 < nk) issue(kt0 + t + NS - 1, (t + NS - 1) % NS);
+    const bool dma = t + NS - 1 < nk;
+    if (dma) issue_prep(kt0 + t + NS - 1, (t + NS - 1) % NS);
+#else
+    const bool dma = false;
 #endif
+    X3S_STAMP(3);
     const bool more = t + 1 < nk;
     if (first_split) {
       if (more) split_a((t + 1) % NS, fn);
+      X3S_STAMP(4);
       __builtin_amdgcn_sched_barrier(0);
-      mma(t % NS);
+      mma(t % NS, dma);
+      X3S_STAMP(5);
     } else {
-      mma(t % NS);
+      mma(t % NS, dma);
+      X3S_STAMP(4);
       __builtin_amdgcn_sched_barrier(0);
       if (more) split_a((t + 1) % NS, fn);
+      X3S_STAMP(5);
     }
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl) fa[pl] = fn[pl];
@@ -1789,3 +1835,9 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
 }
 
 }  // namespace sp
+
+#if SP_X3S_STAMP
+extern "C" int sp_debug_x3s_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sp::g_x3s_stamps), sizeof(sp::g_x3s_stamps));
+}
+#endif
