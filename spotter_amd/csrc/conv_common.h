@@ -242,6 +242,8 @@ __device__ __forceinline__ void epilogue_rowln(const ConvArgs& p, float* tile, c
 // conv_mfma16.hip: bf16-operand MFMA GEMM (planes = 1: bf16; planes = 3: fp32 via a 3-way bf16
 // split). cfg < 0 picks the tile by shape. Returns 0 or the launch error.
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+// The LDS-DMA tile configurations of launch_mfma16 (conv_glds.hip); -2 when cfg is not one of them.
+int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s);
 // Split-K combine kernel launch (conv_gemm.hip).
 int launch_splitk_reduce(const ConvArgs& a, hipStream_t s);
 

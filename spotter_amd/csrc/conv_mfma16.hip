@@ -32,7 +32,7 @@
 
 #include <type_traits>
 
-#include "conv_common.h"
+#include "mfma16_common.h"
 
 #ifndef SP_ABLATE
 #define SP_ABLATE 0
@@ -52,65 +52,6 @@
 namespace sp {
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-
-constexpr int KT = 32;  // k per LDS stage
-
-__device__ __forceinline__ int sw16(int row, int c) { return row * 4 + (c ^ ((row >> 2) & 3)); }
-
-// 8 fp32 → PL bf16 planes (RNE). PL = 3: exact residual chain hi / mid / lo.
-template <int PL>
-__device__ __forceinline__ void split8(const float4& x0, const float4& x1, bf16x8* out) {
-  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-  bf16x8 h, m, l;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    h[j] = (__bf16)v[j];
-    if constexpr (PL == 3) {
-      const float r1 = v[j] - (float)h[j];
-      m[j] = (__bf16)r1;
-      const float r2 = r1 - (float)m[j];
-      l[j] = (__bf16)r2;
-    }
-  }
-  out[0] = h;
-  if constexpr (PL == 3) {
-    out[1] = m;
-    out[2] = l;
-  }
-}
-
-template <int PL>
-__device__ __forceinline__ f32x16 mfma_planes(const bf16x8* a, const bf16x8* b, f32x16 acc) {
-  if constexpr (PL == 1) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-  } else {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-  }
-}
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Same six-product sum on v_mfma_f32_16x16x32_bf16 (one 16×16 block, k = 32 per instruction).
-template <int PL>
-__device__ __forceinline__ f32x4 mfma16x16_planes(const bf16x8* a, const bf16x8* b, f32x4 acc) {
-  if constexpr (PL == 1) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
-  } else {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc, 0, 0, 0);
-  }
-}
 
 template <int WM, int WN, int TM, int TN, int PL, bool FAST>
 __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArgs p) {
@@ -344,318 +285,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
                             lane);
 }
 
-// ---------------------------------------------------------------------------------------------
-// LDS-DMA pipelined variant (no A2 addend, Cin % 32 == 0): every operand byte goes global → LDS
-// by global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), NS stages deep, one raw
-// s_barrier per k-tile and a counted vmcnt that keeps NS-2 stages in flight across it. A is staged
-// as raw fp32 (the k-tile's 32 channels = 8 × 16-byte chunks per im2col row) and split into bf16
-// planes by each wave at fragment-read time, so the split VALU work interleaves with the MFMAs of
-// the same wave instead of sitting between the load wait and the barrier. The DMA destination is
-// lane-linear (wave base + 16·lane), so the bank swizzle is applied on the SOURCE side: LDS chunk
-// position q of A row r holds global chunk q ^ ((r >> 1) & 7) (conflict-free b128 fragment reads,
-// the fp32 kernel's swizzle), position q of a B row holds chunk q ^ ((r >> 2) & 3) (sw16).
-// Padding taps, rows past M and columns past Cout read a 128-byte zero block instead.
-__device__ float4 g_zero_chunk[8];
 #if SP_X3S_STAMP
 __device__ unsigned long long g_x3s_stamps[8 * 64 * 8];
 #endif
-
-template <int PL>
-__device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, bf16x8* out) {
-  split8<PL>(x0, x1, out);
-}
-
-// s_waitcnt vmcnt(n) with expcnt / lgkmcnt left open (gfx9 encoding; n < 64), fenced for the
-// compiler so no LDS access moves across it.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-  asm volatile("" ::: "memory");
-}
-
-// Raw s_barrier (no implied vmcnt(0), unlike __syncthreads), fenced for the compiler.
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// One global_load_lds_dwordx4: 16 bytes from each lane's gsrc to LDS byte address
-// lds_base + 16·lane (lds_base wave-uniform). Issued as inline asm so hipcc does not track it:
-// the builtin form makes hipcc wait vmcnt(0) before every later ds_read of the same array, which
-// drains the stage pipeline; completion is counted by hand (wait_vmcnt + raw_barrier).
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_base)
-      : "memory");
-}
-
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
-__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
-  static_assert(BK == 32 || BK == 16, "k per stage");
-  static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
-  constexpr int NT = 64 * WM * WN;
-  constexpr int BM = 32 * TM * WM;
-  constexpr int BN = 32 * TN * WN;
-  constexpr int RA = BK / 4;  // 16-byte chunks per fp32 A row (8 at BK = 32, 4 at BK = 16)
-  constexpr int RB = BK / 8;  // 16-byte chunks per bf16 B row (4 / 2)
-  constexpr int CA = BM * RA;  // 16-byte chunks of the fp32 A tile
-  constexpr int CB = BN * RB;  // 16-byte chunks of one bf16 B plane
-  constexpr int GA = CA / NT;
-  constexpr int GB = CB / NT;
-  static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
-  constexpr int GLDS = GA + PL * GB;  // DMA instructions per thread per stage
-  constexpr int STAGE = CA + PL * CB;
-  constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
-  constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
-  constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
-  static_assert(NS >= 2 && NS <= 6, "stages");
-  __shared__ uint4 smem[SMEM];
-
-  const sp_conv_desc& d = p.d;
-  const int64_t wps = d.wt_plane_stride;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-
-  const int tilesN = (d.Cout + BN - 1) / BN;
-  const int nwg = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-  const int mt = wg / tilesN;
-  const int n0 = (wg - mt * tilesN) * BN;
-  const int64_t m0 = (int64_t)mt * BM;
-
-  // A pieces: piece j of this thread covers tile row (j·NT + tid) / RA, LDS position tid % RA,
-  // global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of the
-  // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
-  // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
-  const int ca = BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
-  int a_iy0[GA], a_ix0[GA];
-  const float* a_ptr[GA];
-#pragma unroll
-  for (int j = 0; j < GA; ++j) {
-    const int64_t m = m0 + (j * NT + tid) / RA;
-    const bool ok = m < p.M;
-    const int64_t mm = ok ? m : 0;
-    const int b = (int)(mm / p.HoWo);
-    const int rem = (int)(mm - (int64_t)b * p.HoWo);
-    const int oy = rem / d.Wo;
-    const int ox = rem - oy * d.Wo;
-    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
-    a_ix0[j] = ox * d.stride - d.pad;
-    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
-  }
-  // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
-  // (sw16), (row >> 3) & 1 at BK = 16.
-  const int cbk = BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
-  const uint16_t* b_ptr[GB];
-  bool b_ok[GB];
-#pragma unroll
-  for (int j = 0; j < GB; ++j) {
-    const int n = n0 + (j * NT + tid) / RB;
-    b_ok[j] = n < d.Cout;
-    b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
-  }
-  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
-
-  int s_kh = 0, s_kw = 0, s_c0 = 0;
-  const int nk_all = p.K / BK;
-  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
-  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
-  const int nk = kt1 - kt0;
-  {
-    const int k0 = kt0 * BK;
-    const int tap = k0 / d.Cin;
-    s_c0 = k0 - tap * d.Cin;
-    s_kh = tap / d.KW;
-    s_kw = tap - s_kh * d.KW;
-  }
-
-  // Issue the DMA pieces of k-tile kt into stage buffer `buf`, then advance the tap walk.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
-  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-  auto issue = [&](int kt, int buf) {
-    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
-    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
-#pragma unroll
-    for (int j = 0; j < GA; ++j) {
-      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
-      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
-      glds16(src, st + j * NT * 16);
-    }
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int pl = 0; pl < PL; ++pl)
-#pragma unroll
-      for (int j = 0; j < GB; ++j) {
-        const void* src = b_ok[j] ? static_cast<const void*>(b_ptr[j] + pl * wps + k0)
-                                  : static_cast<const void*>(zero + cbk * 16);
-        glds16(src, st + (CA + pl * CB + j * NT) * 16);
-      }
-    s_c0 += BK;
-    if (s_c0 >= d.Cin) {
-      s_c0 = 0;
-      if (++s_kw == d.KW) {
-        s_kw = 0;
-        ++s_kh;
-      }
-    }
-  };
-
-  const int wm = wave / WN;
-  const int wn = wave - wm * WN;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-
-  // M16: each 32×32 block of the wave as 2×2 blocks of v_mfma_f32_16x16x32_bf16 (lane l: A row l & 15,
-  // B column l & 15, k = 8(l >> 4) + j; C rows 4(l >> 4) + reg, column l & 15) on the same LDS images.
-  f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
-  if constexpr (M16) {
-#pragma unroll
-    for (int i = 0; i < 2 * TM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-
-  auto compute = [&](int buf) {
-    const uint4* st = smem + buf * STAGE;
-    if constexpr (M16) {
-      const int c16 = lane & 15, g = lane >> 4;
-      bf16x8 fb[2 * TN][PL];
-#pragma unroll
-      for (int j = 0; j < 2 * TN; ++j) {
-        const int brow = wn * TN * 32 + j * 16 + c16;
-#pragma unroll
-        for (int pl = 0; pl < PL; ++pl)
-          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(brow, g));
-      }
-#pragma unroll
-      for (int i = 0; i < 2 * TM; ++i) {
-        const int row = wm * TM * 32 + i * 16 + c16;
-        const int sz = (row >> 1) & 7;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
-        bf16x8 fa[PL];
-        split_frag<PL>(x0, x1, fa);
-#pragma unroll
-        for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
-      }
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 fb[TN][PL];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int brow = wn * TN * 32 + j * 32 + r;
-        const int bpos = BK == 32 ? sw16(brow, 2 * s + h) : brow * 2 + (h ^ ((brow >> 3) & 1));
-#pragma unroll
-        for (int pl = 0; pl < PL; ++pl)
-          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 32 + i * 32 + r;
-        const int sz = BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
-        const int c0 = 4 * s + 2 * h;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
-        bf16x8 fa[PL];
-#if SP_ABLATE == 2  // no split: one cvt, planes aliased (same MFMA count)
-        {
-          bf16x8 hh;
-          hh[0] = (__bf16)x0.x; hh[1] = (__bf16)x0.y; hh[2] = (__bf16)x0.z; hh[3] = (__bf16)x0.w;
-          hh[4] = (__bf16)x1.x; hh[5] = (__bf16)x1.y; hh[6] = (__bf16)x1.z; hh[7] = (__bf16)x1.w;
-          for (int q = 0; q < PL; ++q) fa[q] = hh;
-        }
-#else
-        split_frag<PL>(x0, x1, fa);
-#endif
-#if SP_ABLATE == 3  // no MFMA: keep the operands alive
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          for (int q = 0; q < PL; ++q) asm volatile("" ::"v"(fa[q]), "v"(fb[j][q]));
-#else
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa, fb[j], acc[i][j]);
-#endif
-      }
-    }
-  };
-
-  // Prologue: stages 0 .. NS-2 in flight.
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue(kt0 + t, t);
-  for (int kt = 0; kt < nk; ++kt) {
-    // retire stage kt: stages kt+1 .. min(kt+NS-2, nk-1) may stay in flight
-    const int ahead = (nk - 1 - kt) < (NS - 2) ? (nk - 1 - kt) : (NS - 2);
-    if (NS >= 6 && ahead >= 4) wait_vmcnt<(NS >= 6 ? 4 * GLDS : 0)>();
-    else if (NS >= 5 && ahead >= 3) wait_vmcnt<(NS >= 5 ? 3 * GLDS : 0)>();
-    else if (NS >= 4 && ahead >= 2) wait_vmcnt<(NS >= 4 ? 2 * GLDS : 0)>();
-    else if (NS >= 3 && ahead >= 1) wait_vmcnt<(NS >= 3 ? GLDS : 0)>();
-    else wait_vmcnt<0>();
-    raw_barrier();
-#if SP_ABLATE == 1  // no DMA in the loop (compute on stale stages)
-    if (false)
-#else
-    if (kt + NS - 1 < nk)
-#endif
-      issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
-    compute(kt % NS);
-  }
-
-  __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
-  float* smemf = reinterpret_cast<float*>(smem);
-  if constexpr (M16) {
-    // 16×16 blocks → the f32x16 of their 32×32 block: element q = 8·bi + 4·bj + reg
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[i][j][q] = acc4[2 * i + (q >> 3)][2 * j + ((q >> 2) & 1)][q & 3];
-  }
-  epilogue_tile<TM, TN, NB, M16>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
-                                 n0 + wn * TN * 32, lane);
-}
-
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
-int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
-  if (a.d.Cin % BK || a.K % BK) {
-    set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
-    return -1;
-  }
-  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
-  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
-  if (tiles > 0x7fffffff) {
-    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
-    return -1;
-  }
-  dim3 grid((unsigned)tiles, 1, a.splits);
-  if (planes == 3)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
-  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
-  if (rc || a.splits == 1) return rc;
-  return launch_splitk_reduce(a, s);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Software-pipelined LDS-DMA variant: as conv_glds_kernel, plus the fragment loads (ds_read +
@@ -1766,39 +1398,8 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     }
   }
   if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 62 && cfg <= 64)) && !a.d.A2) {
-    switch (cfg) {
-      case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
-      case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
-      case 13: return launch_glds<2, 2, 1, 2, 3>(a, planes, s);
-      case 14: return launch_glds<2, 2, 1, 1, 3>(a, planes, s);
-      case 15: return launch_glds<2, 4, 2, 2, 2>(a, planes, s);
-      case 17: return launch_glds<4, 1, 2, 4, 2>(a, planes, s);  // 256×128, 4 waves of 64×128
-      case 18: return launch_glds<2, 2, 2, 4, 2>(a, planes, s);  // 128×256, 4 waves of 64×128
-      case 19: return launch_glds<2, 1, 2, 4, 2>(a, planes, s);  // 128×128, 2 waves of 64×128, 2 stages
-      case 20: return launch_glds<2, 1, 2, 4, 3>(a, planes, s);  // 128×128, 2 waves of 64×128
-      case 33: return launch_glds<4, 2, 2, 4, 2>(a, planes, s);  // 256×256, 8 waves of 64×128
-      case 34: return launch_glds<2, 4, 4, 2, 2>(a, planes, s);  // 256×256, 8 waves of 128×64
-      case 35: return launch_glds<4, 1, 2, 4, 4, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 4 stages
-      case 36: return launch_glds<4, 1, 2, 4, 5, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 5 stages
-      case 37: return launch_glds<4, 2, 2, 4, 3, 16>(a, planes, s);  // 256×256, k16 stages × 3
-      case 38: return launch_glds<4, 2, 2, 4, 4, 16>(a, planes, s);  // 256×256, k16 stages × 4
-      case 41: return launch_glds<4, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 12 on 16x16x32 MFMAs
-      case 42: return launch_glds<4, 2, 2, 4, 2, 32, true>(a, planes, s);  // cfg 33 on 16x16x32 MFMAs
-      case 43: return launch_glds<2, 2, 2, 2, 3, 32, true>(a, planes, s);  // cfg 11 on 16x16x32 MFMAs
-      // two workgroups per CU (LDS <= 80 KB): one's prologue / epilogue hides under the other's MFMAs
-      case 44: return launch_glds<4, 1, 2, 4, 2, 16>(a, planes, s);  // 256×128, 4 waves of 64×128, k16 × 2
-      case 45: return launch_glds<2, 2, 2, 2, 2>(a, planes, s);      // 128×128, k32 × 2 stages
-      case 46: return launch_glds<2, 2, 2, 2, 2, 16>(a, planes, s);  // 128×128, k16 × 2 stages
-      case 48: return launch_glds<2, 2, 2, 4, 2, 16>(a, planes, s);  // 128×256, 4 waves of 64×128, k16 × 2
-      // 64-wide N (Cout = 64 layers): 4 waves of 64×64 stacked along M
-      case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
-      case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
-      // one A row band per wave, the full N width: every A fragment split once per workgroup
-      case 62: return launch_glds<4, 1, 1, 8, 2>(a, planes, s);      // 128×256, 4 waves of 32×256
-      case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
-      case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
-      default: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);
-    }
+    const int rc = launch_glds_cfg(a, planes, cfg, s);
+    if (rc != -2) return rc;
   }
   if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 64 && cfg < 70) || cfg > 75 || (cfg >= 73 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,

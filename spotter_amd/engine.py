@@ -47,6 +47,13 @@ bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack 
 #   "f32"  fp32 MFMA (v_mfma_f32_32x32x2_f32, an exact fmaf chain),
 #   "x3"   fp32 operands as hi/mid/lo bf16 splits on bf16 MFMA (SP_PREC_F32X3; fp32-accurate),
 #   "bf16" bf16 operands, fp32 accumulate (the separately reported bf16 variant).
+# (Cout, K, small_m) layers inside the thin / small-M rule above where the split kernel measured faster
+# than the fp32 MFMA at bs32 (tools/tune_conv.py --cross, profiles/r2/tune_bs32_r101vd_cross_r2.json; each
+# side with its best tile): the stage-0 1×1 expand (0.374 vs 0.401 ms) and the decoder's 9600-row
+# FFN / value / query-pos / box-head linears (1.04-1.26×). Both modes are fp32-accurate.
+_X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256, True), (256, 512, True),
+              (288, 256, True), (4, 256, False)}
+
 PRECISIONS = {
     "fp32": ("x3", "x3"),
     "fp32-mfma": ("f32", "f32"),
@@ -192,6 +199,8 @@ class Engine:
         if mode == "x3" and self.precision == "fp32" and (cout <= 64 or kdim <= 64 or small_m):
             if cout == 64 and kdim >= 576 and not small_m:
                 return mode  # 3×3 64→64 (stage 1): the split kernel's 256×64 tile, 1.09× (conv_bench_thin_x3)
+            if (cout, kdim, small_m) in _X3_FASTER:
+                return mode
             return "f32"
         return mode
 

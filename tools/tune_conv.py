@@ -41,6 +41,16 @@ def geometry(m, cout, K, k, stride):
     return n, h, h, cin
 
 
+_WS = {}
+
+
+def workspace(dev):
+    """The engine's conv workspace (Engine.SPLITK_ELEMS): split-K where the engine would split."""
+    if dev not in _WS:
+        _WS[dev] = torch.empty(16 << 20, device=dev)
+    return _WS[dev]
+
+
 def time_one(dev, m, cout, K, k, stride, mode, cfg, reps):
     n, h, w, cin = geometry(m, cout, K, k, stride)
     pad = k // 2
@@ -57,7 +67,8 @@ def time_one(dev, m, cout, K, k, stride, mode, cfg, reps):
     ops.force_conv_config(None if cfg == "-" else cfg)
 
     def run():
-        ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, stride, pad, view(out, cout), **kw)
+        ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, stride, pad, view(out, cout), workspace=workspace(dev),
+                   **kw)
 
     try:
         for _ in range(2):
@@ -84,7 +95,13 @@ def main():
     ap.add_argument("--min-ms", type=float, default=0.05, help="skip shapes cheaper than this per step")
     ap.add_argument("--steps", type=int, default=10, help="steps the detail file was recorded over")
     ap.add_argument("--modes", default="x3,f32,bf16", help="operand modes to tune")
+    ap.add_argument("--cross", action="store_true",
+                    help="also time f32-mode shapes as x3 and x3-mode shapes as f32 (both fp32-accurate): "
+                         "the per-layer mode choice of Engine._pick")
+    ap.add_argument("--cfgs", default=None, help="comma-separated split / bf16 configurations to time "
+                                                  "(default: all of X3_CFGS)")
     a = ap.parse_args()
+    x3_cfgs = a.cfgs.split(",") if a.cfgs else X3_CFGS
     dev = torch.device("cuda", 0)
     rows = json.load(open(a.detail))
     res = []
@@ -95,13 +112,20 @@ def main():
             continue
         launches = r["launches"] / a.steps
         times = {}
-        for cfg in (F32_CFGS if mode == "f32" else X3_CFGS):
+        for cfg in (F32_CFGS if mode == "f32" else x3_cfgs):
             t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps)
             if t is not None:
                 times[cfg] = round(t, 4)
+        if a.cross and mode in ("f32", "x3"):
+            other = "x3" if mode == "f32" else "f32"
+            for cfg in (F32_CFGS if other == "f32" else x3_cfgs):
+                t = time_one(dev, m, cout, K, k, stride, other, cfg, a.reps)
+                if t is not None:
+                    times[other + ":" + cfg] = round(t, 4)
         best = min(times, key=times.get)
         e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "launches_per_step": launches,
              "default_ms": times.get("-"), "best_cfg": best, "best_ms": times[best], "times": times,
+             "best_same_mode": min((c for c in times if ":" not in c), key=times.get),
              "saving_ms_per_step": round((times.get("-", times[best]) - times[best]) * launches, 4)}
         res.append(e)
         print(json.dumps(e), flush=True)
