@@ -331,12 +331,15 @@ int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     case 44: return launch_glds<4, 1, 2, 4, 2, 16>(a, planes, s);  // 256×128, 4 waves of 64×128, k16 × 2
     case 45: return launch_glds<2, 2, 2, 2, 2>(a, planes, s);      // 128×128, k32 × 2 stages
     case 46: return launch_glds<2, 2, 2, 2, 2, 16>(a, planes, s);  // 128×128, k16 × 2 stages
+    case 47: return launch_glds<2, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 45 on 16x16x32 MFMAs
     case 48: return launch_glds<2, 2, 2, 4, 2, 16>(a, planes, s);  // 128×256, 4 waves of 64×128, k16 × 2
+    case 49: return launch_glds<4, 1, 2, 4, 2, 32, true>(a, planes, s);  // cfg 17 on 16x16x32 MFMAs
     case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
     case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
     case 62: return launch_glds<4, 1, 1, 8, 2>(a, planes, s);      // 128×256, 4 waves of 32×256
     case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
     case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
+    case 65: return launch_glds<8, 1, 1, 4, 2, 32, true>(a, planes, s);  // cfg 63 on 16x16x32 MFMAs
     default: return -2;
   }
 }

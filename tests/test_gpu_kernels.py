@@ -124,7 +124,7 @@ def _bf16(a):
     return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
 
 
-MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "24", "31", "32", "33", "34", "35", "36", "37", "38", "41", "42", "43", "44", "45", "46", "48", "50", "51", "62", "63", "64", "70", "71", "72", "73", "74", "75"]
+MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "21", "24", "31", "32", "33", "34", "35", "36", "37", "38", "41", "42", "43", "44", "45", "46", "47", "48", "49", "50", "51", "62", "63", "64", "65", "70", "71", "72", "73", "74", "75"]
 
 
 @pytest.mark.parametrize("case", CONV_CASES[:7] + [(1, 5, 7, 256, 96, 3, 1, "relu")])
