@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-mfma", "bf16", "bf16-all"],
                     help="GEMM operand precision: fp32 = fp32-accurate 3-way bf16 split GEMMs (SP_PREC_F32X3), "
                          "fp32-mfma = v_mfma_f32_32x32x2_f32 GEMMs; bf16 = the separately reported variant (C3/C4)")
+    ap.add_argument("--winograd", default=None, choices=["off", "auto", "repvgg", "all"],
+                    help="stride-1 3x3 convs as Winograd F(2x2,3x3) (default: the Engine's product default)")
     ap.add_argument("--microbatches", type=int, default=1,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
@@ -78,6 +80,7 @@ CLASS_BOUND = {
     "postprocess": ("hbm", HBM_PEAK_GBS, "GB/s"),
     "layernorm": ("hbm", HBM_PEAK_GBS, "GB/s"),
     "elementwise": ("hbm", HBM_PEAK_GBS, "GB/s"),
+    "wino_tf": ("hbm", HBM_PEAK_GBS, "GB/s"),  # Winograd F(2x2,3x3) input / output transforms
 }
 
 
@@ -362,7 +365,8 @@ def make_step(args, rank, local):
 
     cfg = PRESETS[args.preset].replace(image_size=args.size)
     weights = generate(cfg, seed=0)
-    eng = Engine(cfg, weights, dev, precision=args.precision)
+    ekw = {} if args.winograd is None else {"winograd": False if args.winograd == "off" else args.winograd}
+    eng = Engine(cfg, weights, dev, precision=args.precision, **ekw)
     eng.microbatches = args.microbatches
     eng.stagger = args.stagger
     B, S = args.batch, args.size

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 8
+#define SP_ABI_VERSION 9
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -134,6 +134,29 @@ int sp_conv2d(const sp_conv_desc* d, void* stream);
  * the CALLING THREAD (-1, the default, = chosen by shape). Nothing on the product path calls it, and
  * no environment variable is read: the production tile choice cannot be changed from outside. */
 int sp_set_conv_config(int cfg);
+
+/* 3x3 stride-1 pad-1 convolution by Winograd F(2x2, 3x3) (ABI v9): the same result contract as
+ * sp_conv2d on the same descriptor (KH = KW = 3, stride 1, pad 1; act, scale / shift, res1 / res2 as
+ * above; no A2, row_scale, grouped rows or LayerNorm; Cin % 32 == 0, Cout % 4 == 0, 16-byte aligned
+ * operands), computed as input transform V = B^T d B per 2x2 output tile → 16 batched GEMMs
+ * V_ab · U_ab on the split (SP_PREC_F32X3) or bf16 (SP_PREC_BF16) MFMA kernels → output transform
+ * Y = A^T M A + the fused epilogue. 2.25x fewer GEMM multiply-adds than the implicit GEMM; fp32 error
+ * on par with the direct fp32 conv. wt_wino: the transformed weights U = G g G^T (computed in fp64 on
+ * the host, rounded to fp32) as bf16 planes [planes][16][Cout][Cin] (component ab = 4a + b), planes
+ * wino_plane_stride elements apart (3 planes for SP_PREC_F32X3, 1 for SP_PREC_BF16); d->Wt /
+ * d->Wt_bf16 are not read. work: fp32 scratch of >= 16 * T * (Cin + Cout) elements,
+ * T = N * ceil(H/2) * ceil(W/2). Replaces sp_conv2d for the RepVGG 3x3 (M2:921-923) and other
+ * stride-1 3x3 convs (M2:817-835, RN:78-103). */
+int sp_conv3x3_winograd(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride, float* work,
+                        int64_t work_elems, void* stream);
+/* The three stages of sp_conv3x3_winograd as separate launches (same arguments and checks; work holds
+ * V = work[0 : 16*T*Cin) and M = work[16*T*Cin : 16*T*(Cin+Cout))), so a caller can time the component
+ * GEMM apart from the two HBM-bound transforms: input transform A → V; the 16 batched GEMMs V → M;
+ * output transform + epilogue M → C. */
+int sp_winograd_f23_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream);
+int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride, float* work,
+                         int64_t work_elems, void* stream);
+int sp_winograd_f23_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream);
 
 /* NCHW → NHWC (pixel_values layout of the processor contract → conv layout). */
 int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* stream);

@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -66,6 +66,10 @@ _SIGS = {
     "sp_preprocess_u8": (i32, [C.POINTER(SpImageU8), i32, i32, i32, vp, vp]),
     "sp_conv2d": (i32, [C.POINTER(SpConvDesc), vp]),
     "sp_set_conv_config": (i32, [i32]),
+    "sp_conv3x3_winograd": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
+    "sp_winograd_f23_input": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
+    "sp_winograd_f23_gemm": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
+    "sp_winograd_f23_output": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
     "sp_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "sp_stem_conv3x3s2_nchw": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_maxpool3x3s2": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),

@@ -25,6 +25,12 @@ struct ConvArgs {
   int32_t splits;   // split-K factor (>1: raw partial sums to `partial`, epilogue in splitk_reduce)
   int32_t ldp;      // row stride of a partial slab (Cout rounded up to 4)
   float* partial;   // [splits][M][ldp]
+  // Batched GEMMs (the Winograd component products, winograd.hip): `batch` independent GEMMs of
+  // the same shape whose A / weight planes / C start bs_a / bs_w / bs_c elements apart. Only the
+  // LDS-DMA kernels (conv_glds.hip) take batch > 1; their grid is batch × tiles_per_batch.
+  int32_t batch = 1;
+  int32_t tiles_per_batch = 0;
+  int64_t bs_a = 0, bs_w = 0, bs_c = 0;
 };
 
 // Output row pointer: plain row-major (out_rows_per_group == 0) or grouped rows.
@@ -244,6 +250,8 @@ __device__ __forceinline__ void epilogue_rowln(const ConvArgs& p, float* tile, c
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s);
 // The LDS-DMA tile configurations of launch_mfma16 (conv_glds.hip); -2 when cfg is not one of them.
 int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+// The tile configuration sp_set_conv_config forced for the calling thread (-1: none).
+int forced_cfg();
 // Split-K combine kernel launch (conv_gemm.hip).
 int launch_splitk_reduce(const ConvArgs& a, hipStream_t s);
 

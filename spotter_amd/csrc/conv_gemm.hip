@@ -270,9 +270,10 @@ int launch(const ConvArgs& a, hipStream_t s) {
 // from the environment): "<TM><TN><DB>" for the fp32 kernel (e.g. 221) or the conv_mfma16 config
 // number (bf16 / split kernels); -1 = by shape (the production choice).
 thread_local int g_forced_cfg = -1;
-int forced_cfg() { return g_forced_cfg; }
 
 }  // namespace
+
+int forced_cfg() { return g_forced_cfg; }
 
 int launch_splitk_reduce(const ConvArgs& a, hipStream_t s) {
   int64_t work = a.M * ((a.d.Cout + 3) / 4);

@@ -34,7 +34,7 @@ struct GldsCfg {
 // The LDS-DMA main loop of one output tile: k-tiles [kt0, kt1) of tile `wg` (N fastest) accumulated
 // into acc (acc4 for 16x16x32 MFMAs). The caller zeroes the accumulators and owns the epilogue.
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
-__device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int kt0, int kt1,
+__device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
                                           f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
   static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
@@ -57,6 +57,8 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
   // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
   const int ca = BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
+  const float* A = d.A + (int64_t)bi * p.bs_a;
+  const uint16_t* Wt = d.Wt_bf16 + (int64_t)bi * p.bs_w;
   int a_iy0[GA], a_ix0[GA];
   const float* a_ptr[GA];
 #pragma unroll
@@ -70,7 +72,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     const int ox = rem - oy * d.Wo;
     a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
     a_ix0[j] = ox * d.stride - d.pad;
-    a_ptr[j] = d.A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+    a_ptr[j] = A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
   }
   // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
   // (sw16), (row >> 3) & 1 at BK = 16.
@@ -81,7 +83,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   for (int j = 0; j < GB; ++j) {
     const int n = n0 + (j * NT + tid) / RB;
     b_ok[j] = n < d.Cout;
-    b_ptr[j] = d.Wt_bf16 + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
+    b_ptr[j] = Wt + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
   }
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
 
@@ -239,6 +241,8 @@ __device__ __forceinline__ void glds_zero(f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M
 }
 
 // Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
+// Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
+// index within that member.
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, int wg, f32x16 (&acc)[TM][TN],
                                               f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
@@ -269,16 +273,21 @@ template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
   __shared__ uint4 smem[C::SMEM];
-  const int wg = xcd_index(blockIdx.x, gridDim.x);
+  int wg = xcd_index(blockIdx.x, gridDim.x);
+  // batched launch (Winograd components): member bi owns tiles [bi·tiles_per_batch, (bi+1)·…)
+  const int bi = p.batch > 1 ? wg / p.tiles_per_batch : 0;
+  wg -= bi * p.tiles_per_batch;
   const int nk_all = p.K / BK;
   const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
   const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
   f32x16 acc[TM][TN];
   f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   glds_zero<TM, TN, M16>(acc, acc4);
-  glds_main<WM, WN, TM, TN, PL, NS, BK, M16>(p, smem, wg, kt0, kt1, acc, acc4);
+  glds_main<WM, WN, TM, TN, PL, NS, BK, M16>(p, smem, wg, bi, kt0, kt1, acc, acc4);
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
-  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(p, smem, wg, acc, acc4);
+  ConvArgs q = p;
+  q.d.C += (int64_t)bi * p.bs_c;
+  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(q, smem, wg, acc, acc4);
 }
 
 template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
@@ -288,16 +297,19 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
-  const int64_t tiles = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
-  if (tiles > 0x7fffffff) {
-    set_error("sp_conv2d: %lld tiles exceed the grid", (long long)tiles);
+  const int64_t per = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
+  const int64_t tiles = per * a.batch;
+  if (tiles > 0x7fffffff || (a.batch > 1 && a.splits > 1)) {
+    set_error("sp_conv2d: %lld tiles exceed the grid (or split-K on a batched GEMM)", (long long)tiles);
     return -1;
   }
+  ConvArgs ab = a;
+  ab.tiles_per_batch = (int32_t)per;
   dim3 grid((unsigned)tiles, 1, a.splits);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
   else
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);

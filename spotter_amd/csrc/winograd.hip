@@ -1,0 +1,265 @@
+// 3×3 stride-1 convolution by Winograd F(2×2, 3×3) on the fp32-accurate split GEMM.
+//
+// A 3×3 conv (M2:817-835 ConvNormLayer / M2:921-923 the re-parameterised RepVGG conv, RN:78-103 the
+// ResNet 3×3s) computes out = act(Σ_taps x·w · scale + shift + res1) + res2. With 2×2 output tiles
+// (4×4 input patches d, rows/cols 2t-1 .. 2t+2, zero padding) it factors into
+//   V = Bᵀ d B              (input transform, sp per tile and channel, only ± additions),
+//   M_ab = Σ_ci V_ab · U_ab   (16 independent GEMMs [tiles × Cin] · [Cin × Cout], U = G g Gᵀ on the host),
+//   Y = Aᵀ M A               (output transform, ± additions) → the usual epilogue.
+// The GEMMs carry 16/36 of the direct conv's multiply-adds (2.25× fewer) and run on the batched
+// LDS-DMA kernels of conv_glds.hip in any operand mode (x3 split: fp32-accurate; bf16). In fp32 the
+// transforms add two roundings on each side; the error measured against fp64 matches the direct fp32
+// conv's (the GEMM's K is 9× shorter) — tests/test_gpu_kernels.py::test_winograd_*.
+//
+// Layout: V [16][T][Cin] and M [16][T][Cout] fp32 in the caller's workspace, T = N·⌈H/2⌉·⌈W/2⌉ tiles
+// (b, ty, tx) row-major; component ab = 4a + b. The transform kernels are HBM-bound streams: one
+// thread per (tile, 4 channels), 16 float4 loads, 16 (in) / 4 (out) float4 stores, consecutive
+// threads on consecutive channels.
+#include "conv_common.h"
+
+namespace sp {
+namespace {
+
+__global__ __launch_bounds__(256) void wino_in_f23_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
+                                                          int c4n, int th, int tw, int64_t T,
+                                                          float* __restrict__ V, int64_t cin) {
+  const int64_t total = T * c4n;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = g / c4n;
+    const int c = (int)(g - t * c4n) * 4;
+    const int64_t b = t / ((int64_t)th * tw);
+    const int r = (int)(t - b * th * tw);
+    const int ty = r / tw;
+    const int tx = r - ty * tw;
+    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+    float4 d[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int yy = y0 + i, xx = x0 + j;
+        d[i][j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+                      ? *reinterpret_cast<const float4*>(x + ((b * h + yy) * w + xx) * lda + c)
+                      : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    // rows: r[i][·] = d[i][·] Bᵀ-columns; Bᵀ = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
+    float4 q[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      q[i][0] = d[i][0] - d[i][2];
+      q[i][1] = d[i][1] + d[i][2];
+      q[i][2] = d[i][2] - d[i][1];
+      q[i][3] = d[i][1] - d[i][3];
+    }
+    float* dst = V + t * cin + c;
+    const int64_t plane = T * cin;
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const float4 v0 = q[0][bb] - q[2][bb];
+      const float4 v1 = q[1][bb] + q[2][bb];
+      const float4 v2 = q[2][bb] - q[1][bb];
+      const float4 v3 = q[1][bb] - q[3][bb];
+      *reinterpret_cast<float4*>(dst + (0 * 4 + bb) * plane) = v0;
+      *reinterpret_cast<float4*>(dst + (1 * 4 + bb) * plane) = v1;
+      *reinterpret_cast<float4*>(dst + (2 * 4 + bb) * plane) = v2;
+      *reinterpret_cast<float4*>(dst + (3 * 4 + bb) * plane) = v3;
+    }
+  }
+}
+
+__device__ __forceinline__ float4 epi4(float4 v, const sp_conv_desc& d, int64_t m, int n) {
+  const float4 sc = d.scale ? *reinterpret_cast<const float4*>(d.scale + n) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+  v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y);
+  v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
+  if (d.res1) {
+    const float4 a = *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  v.x = act_apply(v.x, d.act); v.y = act_apply(v.y, d.act);
+  v.z = act_apply(v.z, d.act); v.w = act_apply(v.w, d.act);
+  if (d.res2) {
+    const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restrict__ Mc, int64_t T, int c4n,
+                                                           int th, int tw, const sp_conv_desc d) {
+  const int64_t total = T * c4n;
+  const int64_t cout = d.Cout;
+  const int64_t plane = T * cout;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = g / c4n;
+    const int n = (int)(g - t * c4n) * 4;
+    const int64_t b = t / ((int64_t)th * tw);
+    const int r = (int)(t - b * th * tw);
+    const int ty = r / tw;
+    const int tx = r - ty * tw;
+    const float* src = Mc + t * cout + n;
+    float4 mm[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) mm[a][bb] = *reinterpret_cast<const float4*>(src + (a * 4 + bb) * plane);
+    // Aᵀ = [[1,1,1,0],[0,1,-1,-1]]: s = Aᵀ M (over a), then Y = s A (over b)
+    float4 s[2][4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      s[0][bb] = mm[0][bb] + mm[1][bb] + mm[2][bb];
+      s[1][bb] = mm[1][bb] - mm[2][bb] - mm[3][bb];
+    }
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int oy = 2 * ty + p;
+      if (oy >= d.Ho) break;
+      const float4 y0 = s[p][0] + s[p][1] + s[p][2];
+      const float4 y1 = s[p][1] - s[p][2] - s[p][3];
+      const int64_t m0 = (b * d.Ho + oy) * d.Wo + 2 * tx;
+      *reinterpret_cast<float4*>(d.C + m0 * d.ldc + n) = epi4(y0, d, m0, n);
+      if (2 * tx + 1 < d.Wo) *reinterpret_cast<float4*>(d.C + (m0 + 1) * d.ldc + n) = epi4(y1, d, m0 + 1, n);
+    }
+  }
+}
+
+int stream_grid(int64_t work) {
+  int64_t g = (work + 255) / 256;
+  const int64_t cap = (int64_t)g_num_cus * 16;
+  return (int)(g < cap ? (g > 0 ? g : 1) : cap);
+}
+
+bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
+
+}  // namespace
+}  // namespace sp
+
+namespace sp {
+namespace {
+
+// Validation shared by the Winograd entry points; fills th, tw, T. wt_wino may be null (the
+// transform stages do not read it).
+int wino_check(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+               const float* work, int64_t work_elems, bool need_wt, int* th, int* tw, int64_t* T) {
+  SP_ARG_CHECK(d != nullptr && work != nullptr && (!need_wt || wt_wino != nullptr), "%s: null argument", what);
+  SP_ARG_CHECK(d->A && d->C, "%s: null A/C", what);
+  SP_ARG_CHECK(d->KH == 3 && d->KW == 3 && d->stride == 1 && d->pad == 1 && d->Ho == d->H && d->Wo == d->W,
+               "%s: needs a 3x3 stride-1 pad-1 conv (KH=%d KW=%d stride=%d pad=%d)", what, d->KH, d->KW, d->stride,
+               d->pad);
+  SP_ARG_CHECK(d->N > 0 && d->H > 0 && d->W > 0, "%s: bad shape", what);
+  SP_ARG_CHECK(d->Cin % 32 == 0 && d->Cout % 4 == 0 && d->Cout > 0,
+               "%s: needs Cin %% 32 == 0, Cout %% 4 == 0 (Cin=%d Cout=%d)", what, d->Cin, d->Cout);
+  SP_ARG_CHECK(d->precision == SP_PREC_F32X3 || d->precision == SP_PREC_BF16,
+               "%s: precision %d (split or bf16 operands)", what, d->precision);
+  SP_ARG_CHECK(!d->A2 && !d->row_scale && d->out_rows_per_group == 0 && !d->ln_gamma,
+               "%s: A2 / row_scale / grouped rows / LayerNorm are not supported", what);
+  const int planes = d->precision == SP_PREC_BF16 ? 1 : 3;
+  SP_ARG_CHECK(!need_wt || planes == 1 || wino_plane_stride >= 16LL * d->Cout * d->Cin,
+               "%s: wino_plane_stride %lld < 16*Cout*Cin", what, (long long)wino_plane_stride);
+  SP_ARG_CHECK(d->lda % 4 == 0 && d->ldc % 4 == 0 && al16(d->A) && al16(d->C) && (!need_wt || al16(wt_wino)) &&
+                   (!need_wt || planes == 1 || wino_plane_stride % 8 == 0) &&
+                   (!d->res1 || (d->ldr1 % 4 == 0 && al16(d->res1))) &&
+                   (!d->res2 || (d->ldr2 % 4 == 0 && al16(d->res2))) && (!d->scale || al16(d->scale)) &&
+                   (!d->shift || al16(d->shift)) && al16(work),
+               "%s: operands must be 16-byte aligned with row strides %% 4 == 0", what);
+  *th = (d->H + 1) / 2;
+  *tw = (d->W + 1) / 2;
+  *T = (int64_t)d->N * *th * *tw;
+  SP_ARG_CHECK(*T < 0x7fffffff, "%s: %lld tiles", what, (long long)*T);
+  const int64_t need = 16 * *T * ((int64_t)d->Cin + d->Cout);
+  SP_ARG_CHECK(work_elems >= need, "%s: workspace %lld < %lld elements", what, (long long)work_elems,
+               (long long)need);
+  return 0;
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_winograd_f23_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream) {
+  using namespace sp;
+  int th, tw;
+  int64_t T;
+  if (int rc = wino_check("sp_winograd_f23_input", d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
+  const int cin4 = d->Cin / 4;
+  hipLaunchKernelGGL(wino_in_f23_kernel, dim3(stream_grid(T * cin4)), dim3(256), 0, as_stream(stream), d->A, d->lda,
+                     d->H, d->W, cin4, th, tw, T, work, (int64_t)d->Cin);
+  return check_launch("sp_winograd_f23_input");
+}
+
+extern "C" int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+                                    float* work, int64_t work_elems, void* stream) {
+  using namespace sp;
+  int th, tw;
+  int64_t T;
+  if (int rc = wino_check("sp_winograd_f23_gemm", d, wt_wino, wino_plane_stride, work, work_elems, true, &th, &tw,
+                          &T))
+    return rc;
+  const int planes = d->precision == SP_PREC_BF16 ? 1 : 3;
+  // the 16 component GEMMs as one batched launch: M = T tiles, K = Cin, no epilogue
+  ConvArgs g;
+  memset(&g.d, 0, sizeof(g.d));
+  g.d.A = work;
+  g.d.lda = d->Cin;
+  g.d.N = 1;
+  g.d.H = 1;
+  g.d.W = (int32_t)T;
+  g.d.Cin = d->Cin;
+  g.d.KH = g.d.KW = 1;
+  g.d.stride = 1;
+  g.d.pad = 0;
+  g.d.Ho = 1;
+  g.d.Wo = (int32_t)T;
+  g.d.Cout = d->Cout;
+  g.d.C = work + 16 * T * d->Cin;
+  g.d.ldc = d->Cout;
+  g.d.precision = d->precision;
+  g.d.Wt_bf16 = wt_wino;
+  g.d.wt_plane_stride = wino_plane_stride;
+  g.M = T;
+  g.K = d->Cin;
+  g.HoWo = (int32_t)T;
+  g.fast = 1;
+  g.vec_epi = 1;
+  g.splits = 1;
+  g.ldp = d->Cout;
+  g.partial = nullptr;
+  g.batch = 16;
+  g.bs_a = T * d->Cin;
+  g.bs_w = (int64_t)d->Cout * d->Cin;
+  g.bs_c = T * d->Cout;
+  // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py,
+  // profiles/r2/tune_wino_x3.json: bs32 shapes, 16 × T rows): 256×128 k16 (cfg 44) for the tallest
+  // batches, 128×128 k16 at two workgroups per CU (cfg 46) otherwise, its 16x16x32 form (cfg 47) for
+  // Cout >= 512, 64×64 (cfg 14) when Cout is not a multiple of 128
+  int cfg = forced_cfg();
+  if (cfg < 0) {
+    if (d->Cout % 128) cfg = 14;
+    else if (d->Cout >= 512) cfg = 47;
+    else if (T >= 40000) cfg = 44;
+    else cfg = 46;
+  }
+  const int rc = launch_glds_cfg(g, planes, cfg, as_stream(stream));
+  if (rc == -2) {
+    set_error("sp_winograd_f23_gemm: tile configuration %d is not an LDS-DMA configuration", cfg);
+    return -1;
+  }
+  return rc;
+}
+
+extern "C" int sp_winograd_f23_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
+  using namespace sp;
+  int th, tw;
+  int64_t T;
+  if (int rc = wino_check("sp_winograd_f23_output", d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
+  const int cout4 = d->Cout / 4;
+  hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
+                     work + 16 * T * d->Cin, T, cout4, th, tw, *d);
+  return check_launch("sp_winograd_f23_output");
+}
+
+extern "C" int sp_conv3x3_winograd(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+                                   float* work, int64_t work_elems, void* stream) {
+  if (int rc = sp_winograd_f23_input(d, work, work_elems, stream)) return rc;
+  if (int rc = sp_winograd_f23_gemm(d, wt_wino, wino_plane_stride, work, work_elems, stream)) return rc;
+  return sp_winograd_f23_output(d, work, work_elems, stream);
+}

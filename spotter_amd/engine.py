@@ -72,12 +72,13 @@ def _wkw(wq):
 
 
 class ConvW:
-    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16", "host")
+    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16", "host", "wino")
 
     def __init__(self, w, cin, cout, k, scale, shift, w16=None, host=None):
         self.w, self.cin, self.cout, self.k, self.scale, self.shift = w, cin, cout, k, scale, shift
         self.w16 = w16
         self.host = host  # the packed fp32 [Cout, K] weights on the host (pack-time fusions read them)
+        self.wino = None  # Winograd F(2x2, 3x3) weight planes when this stride-1 3x3 runs that way
 
 
 class LinW:
@@ -141,7 +142,7 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = False):
+                 fuse_ln: bool = False, winograd: str | bool = "auto"):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -154,6 +155,16 @@ class Engine:
         # 42 TF/s (2.47 ms/step) against 1.4 ms/step for the unfused GEMMs + 21 sp_layernorm launches
         # (profiles/r2/fused_ln_ab.json); it stays selectable and tested.
         self.fuse_ln = fuse_ln
+        # stride-1 3x3 convs as Winograd F(2x2, 3x3) (sp_conv3x3_winograd, fp32-accurate on the split GEMM):
+        # "auto" (default) = those with Cin >= 256 on the split operand mode, where it measured 1.25-1.8x
+        # faster than the implicit GEMM at bs32 (tools/tune_wino.py, profiles/r2/tune_wino_x3.json; at
+        # Cin 64 / 128 the transforms cost more than the 2.25x multiply saving); "repvgg" = only the
+        # encoder's folded RepVGG convs; "all" = every stride-1 3x3 on a bf16-operand mode; False = none
+        if winograd is True:
+            winograd = "auto"
+        if winograd not in (False, None, "auto", "repvgg", "all"):
+            raise ValueError("winograd must be False, 'auto', 'repvgg' or 'all'")
+        self.winograd = winograd or False
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
@@ -190,6 +201,22 @@ class Engine:
         if mode == "bf16":
             return torch.from_numpy(bf16_bits(w).view(np.int16)).to(self.dev)
         return torch.from_numpy(ops.split_bf16x3_host(w)).to(self.dev)
+
+    def _add_wino(self, cw: ConvW):
+        """Attach the F(2x2, 3x3) transformed weight planes (host fp64 transform, then the conv's own
+        operand form: three split planes or one bf16 plane) to a stride-1 3x3 conv the Winograd policy
+        (self.winograd) selects."""
+        if cw.k != 3 or cw.w16 is None or cw.cin % 32 or cw.cout % 4 or not self.winograd:
+            return cw
+        planes = cw.w16.shape[0] if cw.w16.dim() == 2 else 1
+        if self.winograd == "auto" and (cw.cin < 256 or planes != 3):
+            return cw
+        u = ops.winograd_weights_host(cw.host.reshape(cw.cout, 3, 3, cw.cin))
+        if planes == 3:
+            cw.wino = torch.from_numpy(ops.split_bf16x3_host(u)).to(self.dev)
+        else:
+            cw.wino = torch.from_numpy(bf16_bits(u).reshape(1, -1).view(np.int16)).to(self.dev)
+        return cw
 
     def _pick(self, mode: str, cout: int, kdim: int, small_m: bool = False) -> str:
         """Per-layer GEMM mode. Under precision "fp32" both operand modes are fp32-accurate, so layers
@@ -245,6 +272,12 @@ class Engine:
             nl = 3 if lt == "bottleneck" else 2
             blk["layers"] = [self._conv(p, f"{pre}.layer.{j}.convolution.weight", f"{pre}.layer.{j}.normalization", True)
                              for j in range(nl)]
+            if self.winograd in ("auto", "all"):
+                # the stride-1 3x3s: bottleneck conv2 (RN:225-231) when the block keeps the resolution,
+                # basic-block conv2 always (RN:170-180)
+                for j, c in enumerate(blk["layers"]):
+                    if c.k == 3 and (st == 1 or (lt != "bottleneck" and j == 1)):
+                        self._add_wino(c)
             if self.fuse_shortcut and lt == "bottleneck" and (sc == "avgconv" or (sc == "conv" and st == 1)):
                 sk = pre + (".shortcut.1" if sc == "avgconv" else ".shortcut")
                 blk["fused"] = self._fused_tail(p, f"{pre}.layer.2", sk, cin)
@@ -336,9 +369,9 @@ class Engine:
                 wf = (w3.astype(np.float64) * s1[:, None, None, None]).copy()
                 wf[:, :, 1, 1] += w1[:, :, 0, 0].astype(np.float64) * s2[:, None]
                 co, ci = w3.shape[:2]
-                reps.append(("fold", self._mk_conv(conv_khwc(wf.astype(np.float32)), ci, co, 3,
-                                                   np.ones(co, np.float32),
-                                                   (b1.astype(np.float64) + b2).astype(np.float32))))
+                cw = self._mk_conv(conv_khwc(wf.astype(np.float32)), ci, co, 3, np.ones(co, np.float32),
+                                   (b1.astype(np.float64) + b2).astype(np.float32))
+                reps.append(("fold", self._add_wino(cw) if self.winograd else cw))
             else:
                 reps.append((self._conv(p, q + ".conv1.conv.weight", q + ".conv1.norm", False),
                              self._conv(p, q + ".conv2.conv.weight", q + ".conv2.norm", False)))
@@ -369,6 +402,11 @@ class Engine:
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
+        if cw.wino is not None and stride == 1 and not kw:
+            tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
+            work = self._buf("wino_work", 16 * tiles * (cw.cin + cw.cout))
+            return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, 3, 1, 1, out, scale=cw.scale, shift=cw.shift,
+                              act=act, res1=res1, res2=res2, wino=(cw.wino, work))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
                           workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)

@@ -206,6 +206,94 @@ def test_conv2d_f32x3_is_fp32_accurate(dev, case, cfg, monkeypatch):
     assert ex3 <= 1e-5 * scale, (ex3, scale)
 
 
+WINO_CASES = [
+    # n, h, w, cin, cout, act
+    (2, 9, 11, 64, 96, "relu"),      # odd H / W: ragged last tile row and column
+    (1, 20, 20, 384, 384, "silu"),   # the CCFM RepVGG shape at 20²
+    (3, 8, 6, 32, 4, None),          # Cout 4 (below every N tile)
+    (1, 1, 1, 32, 64, "gelu"),       # one pixel: a single, mostly padded tile
+    (2, 40, 40, 256, 256, None),     # the backbone stage-3 conv2 shape at bs2
+]
+WINO_CFGS = [None, "63", "33", "14", "45"]
+
+
+@pytest.mark.parametrize("case", WINO_CASES)
+@pytest.mark.parametrize("cfg", WINO_CFGS)
+def test_winograd_f23_is_fp32_accurate(dev, case, cfg):
+    """sp_conv3x3_winograd (F(2x2,3x3): fp32 transforms + the split GEMM) against an fp64 conv of the
+    same fp32 operands: within 2x the fp32 MFMA direct conv's max error (+1e-6 of the output scale) and
+    under 1e-5 of the output scale — the bar of test_conv2d_f32x3_is_fp32_accurate."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    n, h, w, cin, cout, _ = case
+    rng = np.random.default_rng(hash(case) % 2**32 + 5)
+    x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
+    wt = (rng.standard_normal((cout, cin, 3, 3)) / np.sqrt(cin * 9)).astype(np.float32)
+    ref = _conv64(x, wt, 1, 1)
+    m = ref.shape[0]
+    wk_host = wt.transpose(0, 2, 3, 1)
+    wk = T(wk_host.reshape(cout, -1), dev)
+    xd = view(T(x.reshape(-1), dev), cin)
+    out32 = torch.empty(m * cout, device=dev)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, view(out32, cout))
+    planes = T(ops.split_bf16x3_host(ops.winograd_weights_host(wk_host)), dev)
+    tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
+    work = torch.full((16 * tiles * (cin + cout) + 64,), float("nan"), device=dev)
+    out = torch.full((m * cout,), float("nan"), device=dev)
+    ops.force_conv_config(cfg)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, view(out, cout), wino=(planes, work))
+    ops.force_conv_config(None)
+    got = out.cpu().numpy().reshape(m, cout).astype(np.float64)
+    e32 = np.abs(out32.cpu().numpy().reshape(m, cout) - ref).max()
+    ew = np.abs(got - ref).max()
+    scale = np.abs(ref).max()
+    assert np.isfinite(got).all()
+    assert ew <= 2 * e32 + 1e-6 * scale, (ew, e32, scale)
+    assert ew <= 1e-5 * scale, (ew, scale)
+
+
+def test_winograd_epilogue_views_and_bf16(dev):
+    """The Winograd path's epilogue matches the direct conv's: BN scale / shift, res1 (pre-act), act,
+    res2 (post-act), an input channel slice (lda > Cin) and an output slice (ldc > Cout); and the bf16
+    plane form against the bf16-rounded fp64 Winograd product."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(21)
+    n, h, w, cin, cout = 2, 7, 10, 64, 48
+    big = rng.standard_normal((n * h * w, 96)).astype(np.float32)
+    wt = (rng.standard_normal((cout, 3, 3, cin)) / 24).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32)
+    r1 = rng.standard_normal((n * h * w, cout)).astype(np.float32)
+    r2 = rng.standard_normal((n * h * w, cout)).astype(np.float32)
+    m = n * h * w
+    xd = V(T(big.reshape(-1), dev), 16, 96)
+    wk = T(wt.reshape(cout, -1), dev)
+    kw = dict(scale=T(sc, dev), shift=T(sh, dev), act="relu", res1=V(T(r1.reshape(-1), dev), 0, cout),
+              res2=V(T(r2.reshape(-1), dev), 0, cout))
+    ref = torch.zeros(m * 80, device=dev)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(ref, 8, 80), wt_planes=ops.split_bf16x3(wk), **kw)
+    u = ops.winograd_weights_host(wt)
+    tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
+    work = torch.empty(16 * tiles * (cin + cout), device=dev)
+    got = torch.zeros(m * 80, device=dev)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(got, 8, 80), wino=(T(ops.split_bf16x3_host(u), dev), work),
+               **kw)
+    g, r = got.cpu().numpy().reshape(m, 80), ref.cpu().numpy().reshape(m, 80)
+    np.testing.assert_allclose(g[:, 8:8 + cout], r[:, 8:8 + cout], rtol=2e-5, atol=2e-5)
+    assert np.all(g[:, :8] == 0) and np.all(g[:, 8 + cout:] == 0)
+    # bf16 planes: fp32 transforms, bf16-rounded V and U, fp32 accumulate
+    got16 = torch.zeros(m * 80, device=dev)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(got16, 8, 80),
+               wino=(T(ops.bf16_bits(u).reshape(1, -1).view(np.int16), dev), work))
+    plain = torch.zeros(m * cout, device=dev)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(plain, 0, cout))
+    d16 = got16.cpu().numpy().reshape(m, 80)[:, 8:8 + cout] - plain.cpu().numpy().reshape(m, cout)
+    assert np.abs(d16).max() <= 0.05 * np.abs(plain.cpu().numpy()).max(), np.abs(d16).max()
+
+
 def test_conv2d_f32x3_epilogue_and_views(dev):
     """The split path shares the fused epilogue: BN, residuals, act, A2, row mask, grouped rows."""
     from spotter_amd import ops

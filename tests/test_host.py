@@ -68,6 +68,9 @@ def test_arg_errors_are_reported_without_a_gpu():
     assert b"sp_conv2d" in L.sp_last_error()
     assert L.sp_topk_rows(C.c_void_p(16), 0, 1, 100000, 1, 0, 10, None, C.c_void_p(16), None) < 0
     assert b"n=100000" in L.sp_last_error()
+    d = _lib.SpConvDesc(A=16, C=16, KH=3, KW=3, stride=2, pad=1)
+    assert L.sp_conv3x3_winograd(C.byref(d), C.c_void_p(16), 0, C.c_void_p(16), 0, None) < 0
+    assert b"stride-1" in L.sp_last_error()
 
 
 def test_dropin_interface_and_pickling():
@@ -220,6 +223,37 @@ def test_local_checkpoint_round_trip(tmp_path):
     assert cfg2.depths == cfg.depths and cfg2.encoder_hidden_dim == cfg.encoder_hidden_dim
     assert set(w2) == set(w)
     assert all(np.array_equal(w2[k], w[k]) for k in w)
+
+
+def test_winograd_weight_transform_reproduces_the_direct_conv():
+    """ops.winograd_weights_host (U = G g Gᵀ, fp64 on the host) composed with the F(2x2,3x3) input /
+    output transforms the kernels apply (Bᵀ d B, Aᵀ M A; winograd.hip) is the 3x3 stride-1 pad-1
+    cross-correlation: checked in fp64 on a ragged map (odd H, W) against a direct conv."""
+    from spotter_amd import ops
+
+    rng = np.random.default_rng(3)
+    n, h, w, ci, co = 2, 5, 7, 6, 4
+    x = rng.standard_normal((n, h, w, ci))
+    g = rng.standard_normal((co, 3, 3, ci)).astype(np.float32)
+    u = ops.winograd_weights_host(g).astype(np.float64).reshape(4, 4, co, ci)
+    bt = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
+    at = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
+    th, tw = (h + 1) // 2, (w + 1) // 2
+    xp = np.zeros((n, 2 * th + 2, 2 * tw + 2, ci))
+    xp[:, 1:h + 1, 1:w + 1] = x
+    y = np.zeros((n, 2 * th, 2 * tw, co))
+    for ty in range(th):
+        for tx in range(tw):
+            d = xp[:, 2 * ty:2 * ty + 4, 2 * tx:2 * tx + 4]            # [n, 4, 4, ci]
+            v = np.einsum("ai,nijc,bj->nabc", bt, d, bt)
+            m = np.einsum("nabc,aboc->nabo", v, u)
+            y[:, 2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = np.einsum("pa,nabo,qb->npqo", at, m, at)
+    ref = np.zeros((n, h, w, co))
+    xq = np.pad(x, ((0, 0), (1, 1), (1, 1), (0, 0)))
+    for i in range(3):
+        for j in range(3):
+            ref += np.einsum("nhwc,oc->nhwo", xq[:, i:i + h, j:j + w], g[:, i, j, :].astype(np.float64))
+    np.testing.assert_allclose(y[:, :h, :w], ref, rtol=1e-6, atol=1e-5)
 
 
 def test_weight_split_on_host_matches_torch_rne():

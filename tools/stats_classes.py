@@ -11,7 +11,7 @@ import sys
 
 CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "stem_conv")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
            ("attention", ("attn_",)), ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)),
-           ("layernorm", ("layernorm",)), ("postprocess_decode", ("decode_kernel",))]
+           ("layernorm", ("layernorm",)), ("postprocess_decode", ("decode_kernel",)), ("wino_tf", ("wino_",))]
 
 
 def rows(path):
