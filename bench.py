@@ -63,7 +63,7 @@ def parse():
                          "fp32-mfma = v_mfma_f32_32x32x2_f32 GEMMs; bf16 = the separately reported variant (C3/C4)")
     ap.add_argument("--winograd", default=None, choices=["off", "auto", "repvgg", "all"],
                     help="stride-1 3x3 convs as Winograd F(2x2,3x3) (default: the Engine's product default)")
-    ap.add_argument("--microbatches", type=int, default=1,
+    ap.add_argument("--microbatches", type=int, default=None,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU launcher test
@@ -98,17 +98,30 @@ def union_ms(ivs):
     return union
 
 
-class KernelEventRecorder:
-    """HIP events around every kernel launch, recorded on the launch's own stream (the
-    engine makes each micro-batch stream torch's current stream before launching)."""
+# the dominant kernel's operand mode per --precision: the split GEMM (x3) on the fp32 parity path
+DOMINANT_MODE = {"fp32": "x3", "fp32-mfma": "f32", "bf16": "bf16", "bf16-all": "bf16"}
 
-    def __init__(self, torch):
+
+class KernelEventRecorder:
+    """HIP events around kernel launches, recorded on the launch's own stream (the engine makes
+    each micro-batch stream torch's current stream before launching). `only(kind, shape)` limits
+    the events to some launches: every event pair is a marker on the stream that costs the GPU
+    a few microseconds, so the timed region brackets only the dominant kernel's launches (~1/3 of
+    them) and the per-class breakdown comes from a separate, untimed pass with events everywhere."""
+
+    def __init__(self, torch, only=None):
         self.torch = torch
+        self.only = only
         self.recs = []
         self.t0 = torch.cuda.Event(enable_timing=True)
         self.t0.record()
 
+    active = True  # the timed region records during one sampled step only (see main)
+
     def __call__(self, kind, launch, flops, nbytes, shape=None):
+        if not self.active or (self.only is not None and not self.only(kind, shape)):
+            launch()
+            return
         t = self.torch
         e0 = t.cuda.Event(enable_timing=True)
         e1 = t.cuda.Event(enable_timing=True)
@@ -171,7 +184,7 @@ def load_traffic(args, avg_alg_bytes, key="conv"):
         return None, None
     with open(path) as f:
         t = json.load(f)
-    cfg_key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.microbatches}"
+    cfg_key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.mb_eff}"
     e = (t.get(cfg_key) or {}).get("classes", {}).get(key)
     if not e:
         return None, None
@@ -287,11 +300,13 @@ def launch_replicas(args) -> int:
     return rc
 
 
-def conv_roofline(rec, cl, args, bf):
+def conv_roofline(rec, cl, args, bf, rec_timed=None):
     """The dominant kernel's roofline. fp32 (the parity path): the 3-way-split kernel (x3 mode),
     priced against its own pipe ceiling, 2500/6 TF fp32-equivalent (six bf16 MFMAs per fp32
     32x32x16 block); the fp32-MFMA figure stays as a secondary field. Other precisions: the
-    whole conv class against the mode's MFMA peak."""
+    whole conv class against the mode's MFMA peak. rec_timed: the events of the timed region
+    (dominant launches only) — the achieved figure comes from there; rec (every launch, the
+    profiling pass) gives the per-mode and conv-class context."""
     modes = {}
     per_mfma = {"x3": (X3_MFMA_PER_BLOCK, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
                 "bf16": (1, "v_mfma_f32_32x32x16_bf16", BF16_MFMA_PEAK_TFLOPS),
@@ -309,8 +324,11 @@ def conv_roofline(rec, cl, args, bf):
                      "mfma_issue": {"instr": instr, "mfma_per_fp32_block": mult,
                                     "achieved": round(mult * a, 1), "peak": pk, "frac": round(mult * a / pk, 4)}}
     c = cl["conv"]
-    if args.precision == "fp32" and "x3" in cm:
-        x = cm["x3"]
+    timed = rec_timed is not None and bool(rec_timed.recs)
+    cmt = rec_timed.conv_modes() if timed else cm
+    tsteps = 1 if timed else args.steps  # the timed recorder covers one sampled step
+    if args.precision == "fp32" and "x3" in cmt:
+        x = cmt["x3"]
         ach = x["flops"] / (x["ms"] * 1e-3) / 1e12
         alg_bytes = x["bytes"] / x["n"]
         traffic, tnote = load_traffic(args, alg_bytes, key="conv_x3")
@@ -320,7 +338,7 @@ def conv_roofline(rec, cl, args, bf):
                 "frac": round(ach / X3_PEAK_TFLOPS, 4), "traffic": traffic,
                 "peak_note": "fp32-equivalent ceiling of the split kernel = dense bf16 MFMA 2500 TF / 6",
                 "vs_fp32_mfma_peak": {"peak": FP32_MFMA_PEAK_TFLOPS, "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4)},
-                "launches_per_step": x["n"] // args.steps, "avg_launch_ms": round(x["ms"] / x["n"], 4),
+                "launches_per_step": x["n"] // tsteps, "avg_launch_ms": round(x["ms"] / x["n"], 4),
                 "gflop_per_launch": round(x["flops"] / x["n"] / 1e9, 3),
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "flop_share_of_conv_class": round(x["flops"] / max(1, c["flops"]), 4),
@@ -328,8 +346,9 @@ def conv_roofline(rec, cl, args, bf):
                                "ms_per_step": round(c["busy"] / args.steps, 3),
                                "launches_per_step": c["n"] // args.steps,
                                "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2)},
-                "note": "achieved = algorithmic fp32 FLOPs of the x3 launches / the sum of their durations "
-                        "(HIP events on the launch stream); traffic = HBM bytes per x3 launch from PMC "
+                "note": "achieved = algorithmic fp32 FLOPs of the x3 launches (direct convs / linears and the "
+                        "Winograd component GEMMs) / the sum of their durations (HIP events on the launch "
+                        "stream, inside the timed region); traffic = HBM bytes per x3 launch from PMC "
                         "FETCH_SIZE x2 + WRITE_SIZE (MI355X_MICROARCH.md gfx950 correction)"}
     else:
         conv_peak = BF16_MFMA_PEAK_TFLOPS if bf else FP32_MFMA_PEAK_TFLOPS
@@ -367,7 +386,9 @@ def make_step(args, rank, local):
     weights = generate(cfg, seed=0)
     ekw = {} if args.winograd is None else {"winograd": False if args.winograd == "off" else args.winograd}
     eng = Engine(cfg, weights, dev, precision=args.precision, **ekw)
-    eng.microbatches = args.microbatches
+    if args.microbatches is not None:
+        eng.microbatches = args.microbatches
+    args.mb_eff = eng.micro_batches_for(args.batch)
     eng.stagger = args.stagger
     B, S = args.batch, args.size
     imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
@@ -412,17 +433,21 @@ def main():
         step()
     sync()
 
-    rec = None
+    rec, rec_timed = None, None
     if set_hook is not None and not args.no_events:
         import torch
 
-        rec = KernelEventRecorder(torch)
-        set_hook(rec)
+        dom = DOMINANT_MODE[args.precision]
+        rec_timed = KernelEventRecorder(torch, only=lambda k, shp: k == "conv" and bool(shp) and shp[-1] == dom)
+        set_hook(rec_timed)
 
     barrier()
     sync()
+    sample = args.steps // 2  # the timed step whose dominant-kernel launches carry HIP events
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if rec_timed is not None:
+            rec_timed.active = i == sample
         step()
     sync()
     t1 = time.perf_counter()
@@ -437,6 +462,18 @@ def main():
                                "ms_per_step": round(1000 * mine / args.steps, 3)})
     n_img = world * B * args.steps
     value = n_img / elapsed
+
+    if rec_timed is not None:
+        # profiling pass (not timed, not in `value`): events around every launch for the per-class
+        # breakdown, the per-shape detail and the conv-mode context of the roofline
+        import torch
+
+        rec = KernelEventRecorder(torch)
+        set_hook(rec)
+        for _ in range(args.steps):
+            step()
+        sync()
+        set_hook(None)
 
     roof, classes = None, None
     if rec is not None and rec.recs:
@@ -459,7 +496,10 @@ def main():
                     "bytes_per_launch": c["gather"] // c["n"],
                     "note": "sampled-corner bytes (4 taps × Dh × 4 B per sample); the value map stays in L2 / "
                             "Infinity Cache, so the compulsory-bytes figure above is not an HBM bound"}
-        roof = conv_roofline(rec, cl, args, bf)
+        roof = conv_roofline(rec, cl, args, bf, rec_timed)
+        roof["events"] = ("timed region: events around the dominant kernel's launches of one sampled step "
+                          "(step K//2); kernel_classes, modes and conv_class: a separate untimed pass of the "
+                          "same K steps with events on every launch")
 
     if rec is not None and args.detail and rank == 0:
         with open(args.detail, "w") as f:

@@ -186,9 +186,10 @@ class Engine:
         self._consts = {}
         self._ctxs = {}
         self._outs = {}
-        # one stream: the measured fastest at bs32 (profiles/r1/microbatch_ab.json); k > 1 slices on
-        # k streams stay available as Engine.forward(microbatches=k)
-        self.microbatches = 1
+        # None = by batch size (micro_batches_for): two streams from bs16 up, where one slice's GEMM
+        # tails and short-K epilogues overlap the other's main loops (bs32 C2: 629 vs 615 img/s,
+        # profiles/r2/microbatch_ab_r2.json); an int pins it (Engine.forward(microbatches=k) per call)
+        self.microbatches = None
         self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
     # ------------------------------------------------------------------ weights
@@ -628,7 +629,7 @@ class Engine:
         B, C, H, W = pixel_values.shape
         if C != 3:
             raise ValueError("Make sure that the channel dimension of the pixel values match with the one set in the configuration.")
-        nmb = self.microbatches if microbatches is None else microbatches
+        nmb = self.micro_batches_for(B) if microbatches is None else microbatches
         nmb = max(1, min(nmb, B))
         Q, NC = cfg.num_queries, cfg.num_labels
         with torch.cuda.device(self.dev):
@@ -677,6 +678,12 @@ class Engine:
             for i in range(nmb):
                 main.wait_stream(self._ctx(i)["stream"])
             return out_logits, out_boxes
+
+    def micro_batches_for(self, B: int) -> int:
+        """Streams a batch of B images is split over (the served path and bench.py share this)."""
+        if self.microbatches is not None:
+            return self.microbatches
+        return 2 if B >= 16 else 1
 
     def _ctx(self, i):
         c = self._ctxs.get(i)
