@@ -186,9 +186,11 @@ class Engine:
         self._consts = {}
         self._ctxs = {}
         self._outs = {}
-        # None = by batch size (micro_batches_for): two streams from bs16 up, where one slice's GEMM
-        # tails and short-K epilogues overlap the other's main loops (bs32 C2: 629 vs 615 img/s,
-        # profiles/r2/microbatch_ab_r2.json); an int pins it (Engine.forward(microbatches=k) per call)
+        # None = the default split (micro_batches_for: one stream). Two streams measured +1.7 % at bs32
+        # (640 vs 629 img/s, events off; profiles/r2/microbatch_ab_r2.json) but make every kernel share
+        # the chip with the other stream's, so per-kernel durations (the roofline, rocprof) stop
+        # describing the kernels; k > 1 stays available (Engine.forward(microbatches=k) / bench.py
+        # --microbatches k)
         self.microbatches = None
         self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
@@ -683,7 +685,7 @@ class Engine:
         """Streams a batch of B images is split over (the served path and bench.py share this)."""
         if self.microbatches is not None:
             return self.microbatches
-        return 2 if B >= 16 else 1
+        return 1
 
     def _ctx(self, i):
         c = self._ctxs.get(i)

@@ -100,7 +100,7 @@ def run_tiled_batch(preset, reps, precision):
         out = model(**proc(images=imgs, return_tensors="pt").to("cpu"))
     eng = model.engine
     mb = eng.micro_batches_for(n)
-    assert mb == (2 if n >= 16 else 1)  # the bench's own split (bench.py leaves the engine default)
+    assert mb == 1  # the bench's own split (bench.py leaves the engine default)
     tsz = torch.tensor(np.tile(g["target_sizes"], (reps, 1)))
     dets = proc.post_process_object_detection(out, target_sizes=tsz, threshold=0.5)
     if mb == 1:
@@ -114,9 +114,8 @@ def run_tiled_batch(preset, reps, precision):
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
 def test_r101vd_bs32_headline_config_matches_hf_goldens(precision):
-    """C2 exactly as bench.py runs it: R101vd fp32, ONE batch of 32 at 640² on the default split (two
-    micro-batch streams of 16: large-M tile configs, no split-K, XCD remaps over the full grid, Winograd
-    3x3s). The 4 golden images tiled ×8; every
+    """C2 exactly as bench.py runs it: R101vd fp32, ONE batch of 32 at 640² on one stream (large-M tile
+    configs, no split-K, XCD remaps over the full grid, Winograd 3x3s). The 4 golden images tiled ×8; every
     image must meet the parity bar against its HF golden (HF topk M2:1599, post-process IPP:536-576)."""
     model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, precision)
     assert logits.shape == (32, 300, 80)
@@ -180,6 +179,37 @@ def test_r101vd_1280_mixed_resolution_matches_hf_goldens():
         n = int(g["det_counts"][i])
         match_detections(det, g["det_scores"][off:off + n], g["det_labels"][off:off + n], g["det_boxes"][off:off + n])
         off += n
+
+
+def test_two_microbatch_streams_match_one():
+    """Engine.forward(microbatches=2) (two streams, own workspaces) gives the one-stream result (to fp32
+    reassociation: the half-size slices may take other tile / split-K choices)."""
+    import torch
+
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+
+    g = np.load(os.path.join(GOLD, "r18vd_640.npz"))
+    model = SpotterForObjectDetection(PRESETS["r18vd"], use_graphs=False)
+    px = SpotterImageProcessor()(images=load_images(g) * 4, return_tensors="pt")["pixel_values"].to("cuda")
+    eng = model.engine
+    with torch.no_grad():
+        l1, b1 = [t.clone() for t in eng.forward(px, microbatches=1)]
+        l2, b2 = [t.clone() for t in eng.forward(px, microbatches=2)]
+    torch.cuda.synchronize()
+    # fp32 reassociation may swap near-tied anchors in the top-300 query selection (0.6 % of the rows
+    # here), so compare what the deployment returns: the detections above threshold
+    proc = SpotterImageProcessor()
+    from types import SimpleNamespace
+
+    tsz = torch.tensor([[640, 640]] * px.shape[0])
+    d1 = proc.post_process_object_detection(SimpleNamespace(logits=l1, pred_boxes=b1), target_sizes=tsz, threshold=0.5)
+    d2 = proc.post_process_object_detection(SimpleNamespace(logits=l2, pred_boxes=b2), target_sizes=tsz, threshold=0.5)
+    for a, b in zip(d1, d2):
+        assert len(a["scores"]) == len(b["scores"])
+        assert sorted(a["labels"].tolist()) == sorted(b["labels"].tolist())
+        sa, sb = a["scores"].sort().values, b["scores"].sort().values
+        assert (sa - sb).abs().max() <= 1e-3
 
 
 def test_batch_equals_single(tmp_path):

@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--microbatches", type=int, default=None)
     a, _ = ap.parse_known_args()
     if a.microbatches is None:  # the engine's default split (Engine.micro_batches_for)
-        a.microbatches = 2 if a.batch >= 16 else 1
+        a.microbatches = 1
     fe = fold(read(os.path.join(a.outdir, "fetch"), "FETCH_SIZE"))
     wr = fold(read(os.path.join(a.outdir, "write"), "WRITE_SIZE"))
     res = {}
