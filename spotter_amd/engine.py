@@ -158,7 +158,8 @@ class Engine:
         # stride-1 3x3 convs as Winograd F(2x2, 3x3) (sp_conv3x3_winograd, fp32-accurate on the split GEMM):
         # "auto" (default) = those with Cin >= 256 on the split operand mode, where it measured 1.25-1.8x
         # faster than the implicit GEMM at bs32 (tools/tune_wino.py, profiles/r2/tune_wino_x3.json; at
-        # Cin 64 / 128 the transforms cost more than the 2.25x multiply saving); "repvgg" = only the
+        # Cin 64 / 128 the transforms cost more than the 2.25x multiply saving; on bf16 operands it is
+        # always slower, profiles/r2/tune_wino_bf16.json), on maps of >= WINO_MIN_TILES tiles; "repvgg" = only the
         # encoder's folded RepVGG convs; "all" = every stride-1 3x3 on a bf16-operand mode; False = none
         if winograd is True:
             winograd = "auto"
@@ -402,11 +403,14 @@ class Engine:
 
     # ------------------------------------------------------------------ layers
     SPLITK_ELEMS = 16 << 20  # 64 MB fp32 split-K scratch per context
+    WINO_MIN_TILES = 2048
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        if cw.wino is not None and stride == 1 and not kw:
-            tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
+        tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
+        # Winograd only on maps of >= 2048 2x2 tiles: at bs1 the 40² / 20² convs measured 0.69-1.07x of
+        # the split-K implicit GEMM (profiles/r2/tune_wino_x3_bs8_bs1.json), from bs8 up 1.2-1.8x
+        if cw.wino is not None and stride == 1 and not kw and tiles >= self.WINO_MIN_TILES:
             work = self._buf("wino_work", 16 * tiles * (cw.cin + cw.cout))
             return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, 3, 1, 1, out, scale=cw.scale, shift=cw.shift,
                               act=act, res1=res1, res2=res2, wino=(cw.wino, work))
