@@ -324,6 +324,13 @@ def conv_roofline(rec, cl, args, bf, rec_timed=None):
                      "mfma_issue": {"instr": instr, "mfma_per_fp32_block": mult,
                                     "achieved": round(mult * a, 1), "peak": pk, "frac": round(mult * a / pk, 4)}}
     c = cl["conv"]
+    # the convolutions' work in the direct (implicit-GEMM) formulation over the time of every conv-class
+    # launch plus the Winograd transforms: what the Winograd path buys, apart from the kernel's own rate
+    direct_flops = 0
+    for k, e0, e1, f, nb, shp in rec.recs:
+        if k == "conv":
+            direct_flops += (2 * shp[7] * shp[1] * 9 * shp[2]) if (shp and len(shp) > 6 and shp[6] == "wino") else f
+    conv_wino_ms = c["busy"] + cl.get("wino_tf", {}).get("busy", 0.0)
     timed = rec_timed is not None and bool(rec_timed.recs)
     cmt = rec_timed.conv_modes() if timed else cm
     tsteps = 1 if timed else args.steps  # the timed recorder covers one sampled step
@@ -343,6 +350,13 @@ def conv_roofline(rec, cl, args, bf, rec_timed=None):
                 "algorithmic_bytes_per_launch": int(alg_bytes),
                 "flop_share_of_conv_class": round(x["flops"] / max(1, c["flops"]), 4),
                 "conv_class": {"achieved": round(c["flops"] / (c["busy"] * 1e-3) / 1e12, 2),
+                               "direct_equivalent": {
+                                   "tflops": round(direct_flops / (conv_wino_ms * 1e-3) / 1e12, 2),
+                                   "gflop_per_step": round(direct_flops / args.steps / 1e9, 1),
+                                   "ms_per_step": round(conv_wino_ms / args.steps, 3),
+                                   "note": "FLOPs of the direct implicit-GEMM formulation of every conv / linear "
+                                           "over the conv launches + Winograd transforms; counts the 2.25x "
+                                           "multiply saving of the Winograd 3x3s as throughput"},
                                "ms_per_step": round(c["busy"] / args.steps, 3),
                                "launches_per_step": c["n"] // args.steps,
                                "gflop_per_step": round(c["flops"] / args.steps / 1e9, 2)},
@@ -438,7 +452,7 @@ def main():
         import torch
 
         dom = DOMINANT_MODE[args.precision]
-        rec_timed = KernelEventRecorder(torch, only=lambda k, shp: k == "conv" and bool(shp) and shp[-1] == dom)
+        rec_timed = KernelEventRecorder(torch, only=lambda k, shp: k == "conv" and bool(shp) and shp[5] == dom)
         set_hook(rec_timed)
 
     barrier()

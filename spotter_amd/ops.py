@@ -168,7 +168,7 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
                 (m, cin, "in"))
         _launch("conv", "sp_winograd_f23_gemm", (C.byref(d), planes.data_ptr(), planes.shape[1], wp, wn, s),
                 2 * 16 * tiles * cout * cin, 4 * (v_el + m_el) + 2 * planes.numel(),
-                (16 * tiles, cout, cin, 1, 1, "x3" if planes.shape[0] == 3 else "bf16"))
+                (16 * tiles, cout, cin, 1, 1, "x3" if planes.shape[0] == 3 else "bf16", "wino", m))
         _launch("wino_tf", "sp_winograd_f23_output", (C.byref(d), wp, wn, s), 0,
                 4 * (m_el + m * cout * (1 + (res1 is not None) + (res2 is not None))), (m, cout, "out"))
         return ho, wo

@@ -106,7 +106,7 @@ def main():
     rows = json.load(open(a.detail))
     res = []
     for r in rows:
-        m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])
+        m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])[:6]
         per_step = r["ms"] / a.steps
         if mode not in a.modes.split(",") or per_step < a.min_ms:
             continue
