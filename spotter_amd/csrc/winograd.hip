@@ -12,57 +12,69 @@
 // conv's (the GEMM's K is 9× shorter) — tests/test_gpu_kernels.py::test_winograd_*.
 //
 // Layout: V [16][T][Cin] and M [16][T][Cout] fp32 in the caller's workspace, T = N·⌈H/2⌉·⌈W/2⌉ tiles
-// (b, ty, tx) row-major; component ab = 4a + b. The transform kernels are HBM-bound streams: one
-// thread per (tile, 4 channels), 16 float4 loads, 16 (in) / 4 (out) float4 stores, consecutive
-// threads on consecutive channels.
+// (b, ty, tx) row-major; component ab = 4a + b. The transform kernels are HBM-bound streams with
+// consecutive threads on consecutive 4-channel groups: the input transform takes two adjacent tiles
+// per thread (24 float4 loads, 32 float4 stores), the output transform one tile (16 non-temporal
+// float4 loads, 4 float4 stores + the epilogue's residual loads).
 #include "conv_common.h"
 
 namespace sp {
 namespace {
 
-__global__ __launch_bounds__(256) void wino_in_f23_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
-                                                          int c4n, int th, int tw, int64_t T,
-                                                          float* __restrict__ V, int64_t cin) {
-  const int64_t total = T * c4n;
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float4 ld_nt(const float* p) {
+  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// Input transform, two horizontally adjacent tiles per thread: their 4×4 patches share two columns,
+// so 24 loads (4 rows × 6 columns) feed 2 × 16 outputs (profiles/r2/wino_transforms_ab.json: on par
+// with one tile per thread, a little ahead at 80² and 20²; non-temporal V stores measured slower).
+__global__ __launch_bounds__(256) void wino_in_f23_x2_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
+                                                             int c4n, int th, int tw, int64_t nb,
+                                                             float* __restrict__ V, int64_t cin) {
+  const int tw2 = (tw + 1) / 2;
+  const int64_t T = nb * th * tw;
+  const int64_t total = nb * th * tw2 * c4n;
+  const int64_t plane = T * cin;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = g / c4n;
-    const int c = (int)(g - t * c4n) * 4;
-    const int64_t b = t / ((int64_t)th * tw);
-    const int r = (int)(t - b * th * tw);
-    const int ty = r / tw;
-    const int tx = r - ty * tw;
-    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-    float4 d[4][4];
+    const int64_t t2 = g / c4n;
+    const int c = (int)(g - t2 * c4n) * 4;
+    const int64_t b = t2 / ((int64_t)th * tw2);
+    const int r = (int)(t2 - b * th * tw2);
+    const int ty = r / tw2;
+    const int tx0 = 2 * (r - ty * tw2);
+    const int y0 = 2 * ty - 1, x0 = 2 * tx0 - 1;
+    float4 d[4][6];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 6; ++j) {
         const int yy = y0 + i, xx = x0 + j;
         d[i][j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
                       ? *reinterpret_cast<const float4*>(x + ((b * h + yy) * w + xx) * lda + c)
                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-    // rows: r[i][·] = d[i][·] Bᵀ-columns; Bᵀ = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
-    float4 q[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      q[i][0] = d[i][0] - d[i][2];
-      q[i][1] = d[i][1] + d[i][2];
-      q[i][2] = d[i][2] - d[i][1];
-      q[i][3] = d[i][1] - d[i][3];
-    }
-    float* dst = V + t * cin + c;
-    const int64_t plane = T * cin;
+    for (int k = 0; k < 2; ++k) {
+      if (tx0 + k >= tw) break;
+      float4 q[4][4];
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-      const float4 v0 = q[0][bb] - q[2][bb];
-      const float4 v1 = q[1][bb] + q[2][bb];
-      const float4 v2 = q[2][bb] - q[1][bb];
-      const float4 v3 = q[1][bb] - q[3][bb];
-      *reinterpret_cast<float4*>(dst + (0 * 4 + bb) * plane) = v0;
-      *reinterpret_cast<float4*>(dst + (1 * 4 + bb) * plane) = v1;
-      *reinterpret_cast<float4*>(dst + (2 * 4 + bb) * plane) = v2;
-      *reinterpret_cast<float4*>(dst + (3 * 4 + bb) * plane) = v3;
+      for (int i = 0; i < 4; ++i) {
+        q[i][0] = d[i][2 * k + 0] - d[i][2 * k + 2];
+        q[i][1] = d[i][2 * k + 1] + d[i][2 * k + 2];
+        q[i][2] = d[i][2 * k + 2] - d[i][2 * k + 1];
+        q[i][3] = d[i][2 * k + 1] - d[i][2 * k + 3];
+      }
+      float* dst = V + ((b * th + ty) * tw + tx0 + k) * cin + c;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        *reinterpret_cast<float4*>(dst + (0 * 4 + bb) * plane) = q[0][bb] - q[2][bb];
+        *reinterpret_cast<float4*>(dst + (1 * 4 + bb) * plane) = q[1][bb] + q[2][bb];
+        *reinterpret_cast<float4*>(dst + (2 * 4 + bb) * plane) = q[2][bb] - q[1][bb];
+        *reinterpret_cast<float4*>(dst + (3 * 4 + bb) * plane) = q[1][bb] - q[3][bb];
+      }
     }
   }
 }
@@ -102,7 +114,7 @@ __global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restri
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) mm[a][bb] = *reinterpret_cast<const float4*>(src + (a * 4 + bb) * plane);
+      for (int bb = 0; bb < 4; ++bb) mm[a][bb] = ld_nt(src + (a * 4 + bb) * plane);  // read once: +15-20 %
     // Aᵀ = [[1,1,1,0],[0,1,-1,-1]]: s = Aᵀ M (over a), then Y = s A (over b)
     float4 s[2][4];
 #pragma unroll
@@ -181,8 +193,9 @@ extern "C" int sp_winograd_f23_input(const sp_conv_desc* d, float* work, int64_t
   int64_t T;
   if (int rc = wino_check("sp_winograd_f23_input", d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
   const int cin4 = d->Cin / 4;
-  hipLaunchKernelGGL(wino_in_f23_kernel, dim3(stream_grid(T * cin4)), dim3(256), 0, as_stream(stream), d->A, d->lda,
-                     d->H, d->W, cin4, th, tw, T, work, (int64_t)d->Cin);
+const int64_t pairs = (int64_t)d->N * th * ((tw + 1) / 2);
+  hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream), d->A,
+                     d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
   return check_launch("sp_winograd_f23_input");
 }
 

@@ -87,8 +87,33 @@ def main():
             finally:
                 ops.force_conv_config(None)
         best = min(times, key=times.get)
+        # per-stage split of the winning configuration: HIP events around each of the three launches
+        stages = {}
+
+        def hook(kind, launch, flops, nbytes, shape=None):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            launch()
+            e1.record()
+            key = kind if kind == "conv" else f"{kind}:{shape[-1]}"
+            stages.setdefault(key, []).append((e0, e1, nbytes))
+
+        ops.force_conv_config(best)
+        ops.set_launch_hook(hook)
+        try:
+            for _ in range(a.reps):
+                ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, 3, 1, 1, view(out, cout), shift=sh, act="silu",
+                           wino=(planes, work))
+            torch.cuda.synchronize()
+        finally:
+            ops.set_launch_hook(None)
+            ops.force_conv_config(None)
+        split = {}
+        for key, recs in stages.items():
+            ms = sum(e0.elapsed_time(e1) for e0, e1, _ in recs) / len(recs)
+            split[key] = {"ms": round(ms, 4), "GB/s": round(recs[0][2] / (ms * 1e-3) / 1e9, 1)}
         e = {"shape": [n, h, w, cin, cout], "planes": a.planes, "direct_ms": round(direct, 4), "best_cfg": best,
-             "best_ms": times[best], "speedup": round(direct / times[best], 3), "times": times}
+             "best_ms": times[best], "speedup": round(direct / times[best], 3), "stages": split, "times": times}
         res.append(e)
         print(json.dumps(e), flush=True)
     json.dump(res, open(a.out, "w"), indent=1)
