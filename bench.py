@@ -62,7 +62,9 @@ def parse():
                     help="GEMM operand precision: fp32 = fp32-accurate 3-way bf16 split GEMMs (SP_PREC_F32X3), "
                          "fp32-mfma = v_mfma_f32_32x32x2_f32 GEMMs; bf16 = the separately reported variant (C3/C4)")
     ap.add_argument("--winograd", default=None, choices=["off", "auto", "repvgg", "all"],
-                    help="stride-1 3x3 convs as Winograd F(2x2,3x3) (default: the Engine's product default)")
+                    help="stride-1 3x3 convs as Winograd (default: the Engine's product default)")
+    ap.add_argument("--wino-m", type=int, default=None, choices=[2, 4],
+                    help="Winograd output tile: F(2x2,3x3) or F(4x4,3x3) (default: the Engine's)")
     ap.add_argument("--microbatches", type=int, default=None,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
@@ -399,6 +401,8 @@ def make_step(args, rank, local):
     cfg = PRESETS[args.preset].replace(image_size=args.size)
     weights = generate(cfg, seed=0)
     ekw = {} if args.winograd is None else {"winograd": False if args.winograd == "off" else args.winograd}
+    if args.wino_m is not None:
+        ekw["wino_m"] = args.wino_m
     eng = Engine(cfg, weights, dev, precision=args.precision, **ekw)
     if args.microbatches is not None:
         eng.microbatches = args.microbatches

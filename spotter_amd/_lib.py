@@ -70,6 +70,9 @@ _SIGS = {
     "sp_winograd_f23_input": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
     "sp_winograd_f23_gemm": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
     "sp_winograd_f23_output": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
+    "sp_winograd_f43_input": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
+    "sp_winograd_f43_gemm": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
+    "sp_winograd_f43_output": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
     "sp_nchw_to_nhwc": (i32, [vp, vp, i32, i32, i32, i32, vp]),
     "sp_stem_conv3x3s2_nchw": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_maxpool3x3s2": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),

@@ -135,6 +135,153 @@ __global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// F(4×4, 3×3) on the interpolation points (0, -1, 1, ½, -2, ∞): 6×6 input patches (rows / cols
+// 4t-1 .. 4t+4), 36 components, 36/(16·9) = 1/4 of the direct conv's multiply-adds. The points are
+// chosen for fp32 error (numpy study, DESIGN §4: max |e| / Σ|ab| 3.6e-7 vs 1.0e-6 for the common
+// (0, ±1, ±2) set and 7.7e-8 for the direct conv); Bᵀ and Aᵀ hold small dyadic values (exact in fp32),
+// G (thirds, fifteenths) is applied in fp64 on the host. Two channels per thread keep the 6×6 partial
+// sums in ~100 VGPRs.
+constexpr float kBT43[6][6] = {{1.f, -1.5f, -2.f, 1.5f, 1.f, 0.f},  {0.f, 1.f, -2.5f, 0.5f, 1.f, 0.f},
+                               {0.f, -1.f, 0.5f, 2.5f, 1.f, 0.f},   {0.f, -2.f, -1.f, 2.f, 1.f, 0.f},
+                               {0.f, 0.5f, -1.f, -0.5f, 1.f, 0.f},  {0.f, 1.f, -1.5f, -2.f, 1.5f, 1.f}};
+constexpr float kAT43[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                               {0.f, -1.f, 1.f, 0.5f, -2.f, 0.f},
+                               {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
+                               {0.f, -1.f, 1.f, 0.125f, -8.f, 1.f}};
+
+__global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
+                                                          int c2n, int th, int tw, int64_t T,
+                                                          float* __restrict__ V, int64_t cin) {
+  const int64_t total = T * c2n;
+  const int64_t plane = T * cin;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = g / c2n;
+    const int c = (int)(g - t * c2n) * 2;
+    const int64_t b = t / ((int64_t)th * tw);
+    const int r = (int)(t - b * th * tw);
+    const int ty = r / tw;
+    const int tx = r - ty * tw;
+    const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+    float2 q[6][6];  // row pass: q[i][bb] = Σ_j Bᵀ[bb][j] d[i][j]
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float2 dr[6];
+      const int yy = y0 + i;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int xx = x0 + j;
+        dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+                    ? *reinterpret_cast<const float2*>(x + ((b * h + yy) * w + xx) * lda + c)
+                    : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (kBT43[bb][j] != 0.f) {
+            acc.x = fmaf(kBT43[bb][j], dr[j].x, acc.x);
+            acc.y = fmaf(kBT43[bb][j], dr[j].y, acc.y);
+          }
+        q[i][bb] = acc;
+      }
+    }
+    float* dst = V + t * cin + c;
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        float2 v = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int i = 0; i < 6; ++i)
+          if (kBT43[a][i] != 0.f) {
+            v.x = fmaf(kBT43[a][i], q[i][bb].x, v.x);
+            v.y = fmaf(kBT43[a][i], q[i][bb].y, v.y);
+          }
+        *reinterpret_cast<float2*>(dst + (a * 6 + bb) * plane) = v;
+      }
+  }
+}
+
+__device__ __forceinline__ float2 epi2(float2 v, const sp_conv_desc& d, int64_t m, int n) {
+  const float2 sc = d.scale ? *reinterpret_cast<const float2*>(d.scale + n) : make_float2(1.f, 1.f);
+  const float2 sh = d.shift ? *reinterpret_cast<const float2*>(d.shift + n) : make_float2(0.f, 0.f);
+  v.x = fmaf(v.x, sc.x, sh.x);
+  v.y = fmaf(v.y, sc.y, sh.y);
+  if (d.res1) {
+    const float2 a = *reinterpret_cast<const float2*>(d.res1 + m * d.ldr1 + n);
+    v.x += a.x;
+    v.y += a.y;
+  }
+  v.x = act_apply(v.x, d.act);
+  v.y = act_apply(v.y, d.act);
+  if (d.res2) {
+    const float2 a = *reinterpret_cast<const float2*>(d.res2 + m * d.ldr2 + n);
+    v.x += a.x;
+    v.y += a.y;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restrict__ Mc, int64_t T, int c2n,
+                                                           int th, int tw, const sp_conv_desc d) {
+  const int64_t total = T * c2n;
+  const int64_t cout = d.Cout;
+  const int64_t plane = T * cout;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = g / c2n;
+    const int n = (int)(g - t * c2n) * 2;
+    const int64_t b = t / ((int64_t)th * tw);
+    const int r = (int)(t - b * th * tw);
+    const int ty = r / tw;
+    const int tx = r - ty * tw;
+    const float* src = Mc + t * cout + n;
+    float2 s[4][6];  // s[p][bb] = Σ_a Aᵀ[p][a] M[a][bb], accumulated as the rows of M arrive
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) s[p][bb] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float2 mr[6];
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        typedef float v2f __attribute__((ext_vector_type(2)));
+        const v2f v = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(src + (a * 6 + bb) * plane));
+        mr[bb] = make_float2(v.x, v.y);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        if (kAT43[p][a] != 0.f)
+#pragma unroll
+          for (int bb = 0; bb < 6; ++bb) {
+            s[p][bb].x = fmaf(kAT43[p][a], mr[bb].x, s[p][bb].x);
+            s[p][bb].y = fmaf(kAT43[p][a], mr[bb].y, s[p][bb].y);
+          }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int oy = 4 * ty + p;
+      if (oy >= d.Ho) break;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int ox = 4 * tx + qq;
+        if (ox >= d.Wo) break;
+        float2 y = make_float2(0.f, 0.f);
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb)
+          if (kAT43[qq][bb] != 0.f) {
+            y.x = fmaf(kAT43[qq][bb], s[p][bb].x, y.x);
+            y.y = fmaf(kAT43[qq][bb], s[p][bb].y, y.y);
+          }
+        const int64_t m = (b * d.Ho + oy) * d.Wo + ox;
+        *reinterpret_cast<float2*>(d.C + m * d.ldc + n) = epi2(y, d, m, n);
+      }
+    }
+  }
+}
+
 int stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   const int64_t cap = (int64_t)g_num_cus * 16;
@@ -149,10 +296,13 @@ bool al16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
 namespace sp {
 namespace {
 
-// Validation shared by the Winograd entry points; fills th, tw, T. wt_wino may be null (the
-// transform stages do not read it).
+// Validation shared by the Winograd entry points (output tiles MT × MT: 2 for F(2×2,3×3), 4 for
+// F(4×4,3×3); NC = (MT + 2)² components); fills th, tw, T. wt_wino may be null (the transform stages
+// do not read it).
+template <int MT>
 int wino_check(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
                const float* work, int64_t work_elems, bool need_wt, int* th, int* tw, int64_t* T) {
+  constexpr int NC = (MT + 2) * (MT + 2);
   SP_ARG_CHECK(d != nullptr && work != nullptr && (!need_wt || wt_wino != nullptr), "%s: null argument", what);
   SP_ARG_CHECK(d->A && d->C, "%s: null A/C", what);
   SP_ARG_CHECK(d->KH == 3 && d->KW == 3 && d->stride == 1 && d->pad == 1 && d->Ho == d->H && d->Wo == d->W,
@@ -166,49 +316,51 @@ int wino_check(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino,
   SP_ARG_CHECK(!d->A2 && !d->row_scale && d->out_rows_per_group == 0 && !d->ln_gamma,
                "%s: A2 / row_scale / grouped rows / LayerNorm are not supported", what);
   const int planes = d->precision == SP_PREC_BF16 ? 1 : 3;
-  SP_ARG_CHECK(!need_wt || planes == 1 || wino_plane_stride >= 16LL * d->Cout * d->Cin,
-               "%s: wino_plane_stride %lld < 16*Cout*Cin", what, (long long)wino_plane_stride);
+  SP_ARG_CHECK(!need_wt || planes == 1 || wino_plane_stride >= (int64_t)NC * d->Cout * d->Cin,
+               "%s: wino_plane_stride %lld < %d*Cout*Cin", what, (long long)wino_plane_stride, NC);
   SP_ARG_CHECK(d->lda % 4 == 0 && d->ldc % 4 == 0 && al16(d->A) && al16(d->C) && (!need_wt || al16(wt_wino)) &&
                    (!need_wt || planes == 1 || wino_plane_stride % 8 == 0) &&
                    (!d->res1 || (d->ldr1 % 4 == 0 && al16(d->res1))) &&
                    (!d->res2 || (d->ldr2 % 4 == 0 && al16(d->res2))) && (!d->scale || al16(d->scale)) &&
                    (!d->shift || al16(d->shift)) && al16(work),
                "%s: operands must be 16-byte aligned with row strides %% 4 == 0", what);
-  *th = (d->H + 1) / 2;
-  *tw = (d->W + 1) / 2;
+  *th = (d->H + MT - 1) / MT;
+  *tw = (d->W + MT - 1) / MT;
   *T = (int64_t)d->N * *th * *tw;
   SP_ARG_CHECK(*T < 0x7fffffff, "%s: %lld tiles", what, (long long)*T);
-  const int64_t need = 16 * *T * ((int64_t)d->Cin + d->Cout);
+  const int64_t need = (int64_t)NC * *T * ((int64_t)d->Cin + d->Cout);
   SP_ARG_CHECK(work_elems >= need, "%s: workspace %lld < %lld elements", what, (long long)work_elems,
                (long long)need);
   return 0;
 }
 
-}  // namespace
-}  // namespace sp
-
-extern "C" int sp_winograd_f23_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream) {
-  using namespace sp;
+template <int MT>
+int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t work_elems, void* stream) {
   int th, tw;
   int64_t T;
-  if (int rc = wino_check("sp_winograd_f23_input", d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
-  const int cin4 = d->Cin / 4;
-const int64_t pairs = (int64_t)d->N * th * ((tw + 1) / 2);
-  hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream), d->A,
-                     d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
-  return check_launch("sp_winograd_f23_input");
+  if (int rc = wino_check<MT>(what, d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
+  if constexpr (MT == 2) {
+    const int cin4 = d->Cin / 4;
+    const int64_t pairs = (int64_t)d->N * th * ((tw + 1) / 2);
+    hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream),
+                       d->A, d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
+  } else {
+    const int cin2 = d->Cin / 2;
+    hipLaunchKernelGGL(wino_in_f43_kernel, dim3(stream_grid(T * cin2)), dim3(256), 0, as_stream(stream), d->A,
+                       d->lda, d->H, d->W, cin2, th, tw, T, work, (int64_t)d->Cin);
+  }
+  return check_launch(what);
 }
 
-extern "C" int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
-                                    float* work, int64_t work_elems, void* stream) {
-  using namespace sp;
+template <int MT>
+int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+              float* work, int64_t work_elems, void* stream) {
+  constexpr int NC = (MT + 2) * (MT + 2);
   int th, tw;
   int64_t T;
-  if (int rc = wino_check("sp_winograd_f23_gemm", d, wt_wino, wino_plane_stride, work, work_elems, true, &th, &tw,
-                          &T))
-    return rc;
+  if (int rc = wino_check<MT>(what, d, wt_wino, wino_plane_stride, work, work_elems, true, &th, &tw, &T)) return rc;
   const int planes = d->precision == SP_PREC_BF16 ? 1 : 3;
-  // the 16 component GEMMs as one batched launch: M = T tiles, K = Cin, no epilogue
+  // the NC component GEMMs as one batched launch: M = T tiles, K = Cin, no epilogue
   ConvArgs g;
   memset(&g.d, 0, sizeof(g.d));
   g.d.A = work;
@@ -223,7 +375,7 @@ extern "C" int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wi
   g.d.Ho = 1;
   g.d.Wo = (int32_t)T;
   g.d.Cout = d->Cout;
-  g.d.C = work + 16 * T * d->Cin;
+  g.d.C = work + NC * T * d->Cin;
   g.d.ldc = d->Cout;
   g.d.precision = d->precision;
   g.d.Wt_bf16 = wt_wino;
@@ -236,38 +388,61 @@ extern "C" int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wi
   g.splits = 1;
   g.ldp = d->Cout;
   g.partial = nullptr;
-  g.batch = 16;
+  g.batch = NC;
   g.bs_a = T * d->Cin;
   g.bs_w = (int64_t)d->Cout * d->Cin;
   g.bs_c = T * d->Cout;
   // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py,
-  // profiles/r2/tune_wino_x3.json: bs32 shapes, 16 × T rows): 256×128 k16 (cfg 44) for the tallest
+  // profiles/r2/tune_wino_x3.json: bs32 shapes, NC × T rows): 256×128 k16 (cfg 44) for the tallest
   // batches, 128×128 k16 at two workgroups per CU (cfg 46) otherwise, its 16x16x32 form (cfg 47) for
   // Cout >= 512, 64×64 (cfg 14) when Cout is not a multiple of 128
   int cfg = forced_cfg();
   if (cfg < 0) {
     if (d->Cout % 128) cfg = 14;
     else if (d->Cout >= 512) cfg = 47;
-    else if (T >= 40000) cfg = 44;
+    else if (T * NC >= 640000) cfg = 44;
     else cfg = 46;
   }
   const int rc = launch_glds_cfg(g, planes, cfg, as_stream(stream));
   if (rc == -2) {
-    set_error("sp_winograd_f23_gemm: tile configuration %d is not an LDS-DMA configuration", cfg);
+    set_error("%s: tile configuration %d is not an LDS-DMA configuration", what, cfg);
     return -1;
   }
   return rc;
 }
 
-extern "C" int sp_winograd_f23_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
-  using namespace sp;
+template <int MT>
+int wino_output(const char* what, const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
+  constexpr int NC = (MT + 2) * (MT + 2);
   int th, tw;
   int64_t T;
-  if (int rc = wino_check("sp_winograd_f23_output", d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
-  const int cout4 = d->Cout / 4;
-  hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
-                     work + 16 * T * d->Cin, T, cout4, th, tw, *d);
-  return check_launch("sp_winograd_f23_output");
+  if (int rc = wino_check<MT>(what, d, nullptr, 0, work, work_elems, false, &th, &tw, &T)) return rc;
+  if constexpr (MT == 2) {
+    const int cout4 = d->Cout / 4;
+    hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
+                       work + NC * T * d->Cin, T, cout4, th, tw, *d);
+  } else {
+    const int cout2 = d->Cout / 2;
+    hipLaunchKernelGGL(wino_out_f43_kernel, dim3(stream_grid(T * cout2)), dim3(256), 0, as_stream(stream),
+                       work + NC * T * d->Cin, T, cout2, th, tw, *d);
+  }
+  return check_launch(what);
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_winograd_f23_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream) {
+  return sp::wino_input<2>("sp_winograd_f23_input", d, work, work_elems, stream);
+}
+
+extern "C" int sp_winograd_f23_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+                                    float* work, int64_t work_elems, void* stream) {
+  return sp::wino_gemm<2>("sp_winograd_f23_gemm", d, wt_wino, wino_plane_stride, work, work_elems, stream);
+}
+
+extern "C" int sp_winograd_f23_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
+  return sp::wino_output<2>("sp_winograd_f23_output", d, work, work_elems, stream);
 }
 
 extern "C" int sp_conv3x3_winograd(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
@@ -275,4 +450,17 @@ extern "C" int sp_conv3x3_winograd(const sp_conv_desc* d, const uint16_t* wt_win
   if (int rc = sp_winograd_f23_input(d, work, work_elems, stream)) return rc;
   if (int rc = sp_winograd_f23_gemm(d, wt_wino, wino_plane_stride, work, work_elems, stream)) return rc;
   return sp_winograd_f23_output(d, work, work_elems, stream);
+}
+
+extern "C" int sp_winograd_f43_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream) {
+  return sp::wino_input<4>("sp_winograd_f43_input", d, work, work_elems, stream);
+}
+
+extern "C" int sp_winograd_f43_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
+                                    float* work, int64_t work_elems, void* stream) {
+  return sp::wino_gemm<4>("sp_winograd_f43_gemm", d, wt_wino, wino_plane_stride, work, work_elems, stream);
+}
+
+extern "C" int sp_winograd_f43_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
+  return sp::wino_output<4>("sp_winograd_f43_output", d, work, work_elems, stream);
 }

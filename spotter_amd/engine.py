@@ -142,7 +142,7 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = False, winograd: str | bool = "auto"):
+                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -155,17 +155,22 @@ class Engine:
         # 42 TF/s (2.47 ms/step) against 1.4 ms/step for the unfused GEMMs + 21 sp_layernorm launches
         # (profiles/r2/fused_ln_ab.json); it stays selectable and tested.
         self.fuse_ln = fuse_ln
-        # stride-1 3x3 convs as Winograd F(2x2, 3x3) (sp_conv3x3_winograd, fp32-accurate on the split GEMM):
-        # "auto" (default) = those with Cin >= 256 on the split operand mode, where it measured 1.25-1.8x
-        # faster than the implicit GEMM at bs32 (tools/tune_wino.py, profiles/r2/tune_wino_x3.json; at
-        # Cin 64 / 128 the transforms cost more than the 2.25x multiply saving; on bf16 operands it is
-        # always slower, profiles/r2/tune_wino_bf16.json), on maps of >= WINO_MIN_TILES tiles; "repvgg" = only the
-        # encoder's folded RepVGG convs; "all" = every stride-1 3x3 on a bf16-operand mode; False = none
+        # stride-1 3x3 convs as Winograd F(m x m, 3x3) on the split GEMM (sp_winograd_f{2,4}3_*): "auto"
+        # (default) = those on the split operand mode with Cin >= 128 for F(4x4) (1.4-2.6x faster than the
+        # implicit GEMM at bs32, profiles/r2/tune_wino_f43_x3.json) or Cin >= 256 for F(2x2) (1.25-1.8x,
+        # profiles/r2/tune_wino_x3.json; below that the transforms cost more than the multiply saving; on
+        # bf16 operands it is always slower, profiles/r2/tune_wino_bf16.json), on maps of >= WINO_MIN_PIXELS
+        # pixels; "repvgg" = only the encoder's folded RepVGG convs; "all" = every stride-1 3x3 on a
+        # bf16-operand mode; False = none. wino_m = 4 (default, 1/4 of the direct multiply-adds, fp32 error
+        # 3-5x the direct conv's) or 2 (4/9, error on par with the direct conv).
         if winograd is True:
             winograd = "auto"
         if winograd not in (False, None, "auto", "repvgg", "all"):
             raise ValueError("winograd must be False, 'auto', 'repvgg' or 'all'")
         self.winograd = winograd or False
+        if wino_m not in (2, 4):
+            raise ValueError("wino_m must be 2 (F(2x2,3x3)) or 4 (F(4x4,3x3))")
+        self.wino_m = wino_m
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
@@ -213,9 +218,9 @@ class Engine:
         if cw.k != 3 or cw.w16 is None or cw.cin % 32 or cw.cout % 4 or not self.winograd:
             return cw
         planes = cw.w16.shape[0] if cw.w16.dim() == 2 else 1
-        if self.winograd == "auto" and (cw.cin < 256 or planes != 3):
+        if self.winograd == "auto" and (cw.cin < (128 if self.wino_m == 4 else 256) or planes != 3):
             return cw
-        u = ops.winograd_weights_host(cw.host.reshape(cw.cout, 3, 3, cw.cin))
+        u = ops.winograd_weights_host(cw.host.reshape(cw.cout, 3, 3, cw.cin), self.wino_m)
         if planes == 3:
             cw.wino = torch.from_numpy(ops.split_bf16x3_host(u)).to(self.dev)
         else:
@@ -403,17 +408,19 @@ class Engine:
 
     # ------------------------------------------------------------------ layers
     SPLITK_ELEMS = 16 << 20  # 64 MB fp32 split-K scratch per context
-    WINO_MIN_TILES = 2048
+    WINO_MIN_PIXELS = 8192
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
-        # Winograd only on maps of >= 2048 2x2 tiles: at bs1 the 40² / 20² convs measured 0.69-1.07x of
-        # the split-K implicit GEMM (profiles/r2/tune_wino_x3_bs8_bs1.json), from bs8 up 1.2-1.8x
-        if cw.wino is not None and stride == 1 and not kw and tiles >= self.WINO_MIN_TILES:
-            work = self._buf("wino_work", 16 * tiles * (cw.cin + cw.cout))
+        # Winograd only on maps of >= 8192 output pixels (2048 2x2 tiles): at bs1 the 40² / 20² convs
+        # measured 0.69-1.07x of the split-K implicit GEMM (profiles/r2/tune_wino_x3_bs8_bs1.json), from
+        # bs8 up 1.2-1.8x
+        if cw.wino is not None and stride == 1 and not kw and n * h * w >= self.WINO_MIN_PIXELS:
+            wm = self.wino_m
+            tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
+            work = self._buf("wino_work", (wm + 2) ** 2 * tiles * (cw.cin + cw.cout))
             return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, 3, 1, 1, out, scale=cw.scale, shift=cw.shift,
-                              act=act, res1=res1, res2=res2, wino=(cw.wino, work))
+                              act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
                           workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)

@@ -73,9 +73,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
            wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None):
     """ln = (gamma, beta, eps): LayerNorm over each output row fused into the epilogue (fp32 weights).
-    wino = (planes, work): run this 3×3 stride-1 conv as Winograd F(2×2, 3×3) (sp_conv3x3_winograd) on
-    the transformed weight planes (int16 [3 or 1, 16·Cout·Cin], winograd_weights_host + split) with the
-    fp32 scratch `work`; the bf16 / split operand mode follows the plane count.
+    wino = (planes, work[, m]): run this 3×3 stride-1 conv as Winograd F(m×m, 3×3), m = 2 (default) or 4
+    (sp_winograd_f23_* / _f43_*), on the transformed weight planes (int16 [3 or 1, (m+2)²·Cout·Cin],
+    winograd_weights_host + split) with the fp32 scratch `work`; the bf16 / split operand mode follows the
+    plane count.
     wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
     wt_planes (int16 [3, Cout*K]: the hi / mid / lo bf16 split of the fp32 weights, split_bf16x3)
     selects the fp32-accurate 3-way-split path (SP_PREC_F32X3)."""
@@ -149,27 +150,31 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     nbytes = 4 * (n * h * w * cin * (2 if a2 is not None else 1) + cout * k * k * cin + m * cout
                   * (1 + (res1 is not None) + (res2 is not None)))
     if wino is not None:
-        planes, work = wino
+        planes, work = wino[0], wino[1]
+        wm = wino[2] if len(wino) > 2 else 2
+        nc = (wm + 2) ** 2
         if k != 3 or stride != 1 or pad != 1 or ln is not None or a2 is not None:
             raise ValueError("conv: Winograd needs a 3x3 stride-1 pad-1 conv without A2 / LayerNorm")
-        if (planes.dim() != 2 or planes.shape[0] not in (1, 3) or planes.shape[1] != 16 * cout * cin
+        if wm not in (2, 4):
+            raise ValueError("conv: Winograd tile must be 2 or 4")
+        if (planes.dim() != 2 or planes.shape[0] not in (1, 3) or planes.shape[1] != nc * cout * cin
                 or planes.dtype != torch.int16 or not planes.is_contiguous() or not planes.is_cuda):
-            raise ValueError("conv: Winograd weight planes must be int16 [1 or 3, 16*Cout*Cin]")
-        tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
-        if work.dtype != torch.float32 or not work.is_cuda or work.numel() < 16 * tiles * (cin + cout):
+            raise ValueError(f"conv: Winograd weight planes must be int16 [1 or 3, {nc}*Cout*Cin]")
+        tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
+        if work.dtype != torch.float32 or not work.is_cuda or work.numel() < nc * tiles * (cin + cout):
             raise ValueError("conv: Winograd workspace too small")
         d.precision = 2 if planes.shape[0] == 3 else 1
         d.Wt_bf16 = None
         # three launches (sp_winograd_f23_input / _gemm / _output) so the launch hook times the component
         # GEMM, a batched 1x1 GEMM of 16·T rows in the conv's operand mode, apart from the transforms
         wp, wn, s = work.data_ptr(), work.numel(), stream()
-        v_el, m_el = 16 * tiles * cin, 16 * tiles * cout
-        _launch("wino_tf", "sp_winograd_f23_input", (C.byref(d), wp, wn, s), 0, 4 * (n * h * w * cin + v_el),
-                (m, cin, "in"))
-        _launch("conv", "sp_winograd_f23_gemm", (C.byref(d), planes.data_ptr(), planes.shape[1], wp, wn, s),
-                2 * 16 * tiles * cout * cin, 4 * (v_el + m_el) + 2 * planes.numel(),
-                (16 * tiles, cout, cin, 1, 1, "x3" if planes.shape[0] == 3 else "bf16", "wino", m))
-        _launch("wino_tf", "sp_winograd_f23_output", (C.byref(d), wp, wn, s), 0,
+        v_el, m_el = nc * tiles * cin, nc * tiles * cout
+        f = f"sp_winograd_f{wm}3"
+        _launch("wino_tf", f + "_input", (C.byref(d), wp, wn, s), 0, 4 * (n * h * w * cin + v_el), (m, cin, "in"))
+        _launch("conv", f + "_gemm", (C.byref(d), planes.data_ptr(), planes.shape[1], wp, wn, s),
+                2 * nc * tiles * cout * cin, 4 * (v_el + m_el) + 2 * planes.numel(),
+                (nc * tiles, cout, cin, 1, 1, "x3" if planes.shape[0] == 3 else "bf16", "wino", m))
+        _launch("wino_tf", f + "_output", (C.byref(d), wp, wn, s), 0,
                 4 * (m_el + m * cout * (1 + (res1 is not None) + (res2 is not None))), (m, cout, "out"))
         return ho, wo
     _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
@@ -207,16 +212,30 @@ def split_bf16x3_host(w) -> np.ndarray:
     return np.stack([hi, mid, lo]).view(np.int16)
 
 
-def winograd_weights_host(wk) -> np.ndarray:
-    """3×3 conv weights [Cout][3][3][Cin] (host fp32) → the F(2×2, 3×3) transformed weights
-    U_ab = G g Gᵀ as fp32 [16][Cout][Cin] (component ab = 4a + b), computed in fp64 and rounded once;
-    G = [[1, 0, 0], [½, ½, ½], [½, -½, ½], [0, 0, 1]] (sp_conv3x3_winograd)."""
+# Winograd F(m×m, 3×3) transform matrices (winograd.hip): F(2×2) on the points (0, 1, -1, ∞); F(4×4) on
+# (0, -1, 1, ½, -2, ∞), chosen for fp32 error. Bᵀ and Aᵀ are what the kernels apply (dyadic, exact in fp32);
+# G is applied here in fp64.
+WINO_BT = {2: np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64),
+           4: np.array([[1, -1.5, -2, 1.5, 1, 0], [0, 1, -2.5, 0.5, 1, 0], [0, -1, 0.5, 2.5, 1, 0],
+                        [0, -2, -1, 2, 1, 0], [0, 0.5, -1, -0.5, 1, 0], [0, 1, -1.5, -2, 1.5, 1]], np.float64)}
+WINO_AT = {2: np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64),
+           4: np.array([[1, 1, 1, 1, 1, 0], [0, -1, 1, 0.5, -2, 0], [0, 1, 1, 0.25, 4, 0],
+                        [0, -1, 1, 0.125, -8, 1]], np.float64)}
+WINO_G = {2: np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], np.float64),
+          4: np.array([[1, 0, 0], [-1 / 3, 1 / 3, -1 / 3], [1 / 3, 1 / 3, 1 / 3], [-16 / 15, -8 / 15, -4 / 15],
+                       [1 / 15, -2 / 15, 4 / 15], [0, 0, 1]], np.float64)}
+
+
+def winograd_weights_host(wk, m: int = 2) -> np.ndarray:
+    """3×3 conv weights [Cout][3][3][Cin] (host fp32) → the F(m×m, 3×3) transformed weights U_ab = G g Gᵀ
+    as fp32 [(m+2)², Cout, Cin] (component ab = (m+2)·a + b), computed in fp64 and rounded once
+    (sp_winograd_f23_* / sp_winograd_f43_*)."""
     g = np.asarray(wk, dtype=np.float64)
     if g.ndim != 4 or g.shape[1:3] != (3, 3):
         raise ValueError(f"winograd weights: expected [Cout, 3, 3, Cin], got {g.shape}")
-    G = np.array([[1, 0, 0], [.5, .5, .5], [.5, -.5, .5], [0, 0, 1]], dtype=np.float64)
+    G = WINO_G[m]
     u = np.einsum("ai,oijc,bj->aboc", G, g, G)
-    return np.ascontiguousarray(u.reshape(16, g.shape[0], g.shape[3]).astype(np.float32))
+    return np.ascontiguousarray(u.reshape((m + 2) ** 2, g.shape[0], g.shape[3]).astype(np.float32))
 
 
 def split_bf16x3(w: torch.Tensor) -> torch.Tensor:

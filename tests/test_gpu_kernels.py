@@ -219,8 +219,9 @@ WINO_CFGS = [None, "63", "33", "14", "45"]
 
 @pytest.mark.parametrize("case", WINO_CASES)
 @pytest.mark.parametrize("cfg", WINO_CFGS)
-def test_winograd_f23_is_fp32_accurate(dev, case, cfg):
-    """sp_conv3x3_winograd (F(2x2,3x3): fp32 transforms + the split GEMM) against an fp64 conv of the
+@pytest.mark.parametrize("wm", [2, 4])
+def test_winograd_is_fp32_accurate(dev, case, cfg, wm):
+    """sp_winograd_f{2,4}3_* (F(m×m,3x3): fp32 transforms + the split GEMM) against an fp64 conv of the
     same fp32 operands: within 2x the fp32 MFMA direct conv's max error (+1e-6 of the output scale) and
     under 1e-5 of the output scale — the bar of test_conv2d_f32x3_is_fp32_accurate."""
     from spotter_amd import ops
@@ -237,12 +238,12 @@ def test_winograd_f23_is_fp32_accurate(dev, case, cfg):
     xd = view(T(x.reshape(-1), dev), cin)
     out32 = torch.empty(m * cout, device=dev)
     ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, view(out32, cout))
-    planes = T(ops.split_bf16x3_host(ops.winograd_weights_host(wk_host)), dev)
-    tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
-    work = torch.full((16 * tiles * (cin + cout) + 64,), float("nan"), device=dev)
+    planes = T(ops.split_bf16x3_host(ops.winograd_weights_host(wk_host, wm)), dev)
+    tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
+    work = torch.full(((wm + 2) ** 2 * tiles * (cin + cout) + 64,), float("nan"), device=dev)
     out = torch.full((m * cout,), float("nan"), device=dev)
     ops.force_conv_config(cfg)
-    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, view(out, cout), wino=(planes, work))
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, view(out, cout), wino=(planes, work, wm))
     ops.force_conv_config(None)
     got = out.cpu().numpy().reshape(m, cout).astype(np.float64)
     e32 = np.abs(out32.cpu().numpy().reshape(m, cout) - ref).max()
@@ -253,7 +254,8 @@ def test_winograd_f23_is_fp32_accurate(dev, case, cfg):
     assert ew <= 1e-5 * scale, (ew, scale)
 
 
-def test_winograd_epilogue_views_and_bf16(dev):
+@pytest.mark.parametrize("wm", [2, 4])
+def test_winograd_epilogue_views_and_bf16(dev, wm):
     """The Winograd path's epilogue matches the direct conv's: BN scale / shift, res1 (pre-act), act,
     res2 (post-act), an input channel slice (lda > Cin) and an output slice (ldc > Cout); and the bf16
     plane form against the bf16-rounded fp64 Winograd product."""
@@ -275,19 +277,19 @@ def test_winograd_epilogue_views_and_bf16(dev):
               res2=V(T(r2.reshape(-1), dev), 0, cout))
     ref = torch.zeros(m * 80, device=dev)
     ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(ref, 8, 80), wt_planes=ops.split_bf16x3(wk), **kw)
-    u = ops.winograd_weights_host(wt)
-    tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
-    work = torch.empty(16 * tiles * (cin + cout), device=dev)
+    u = ops.winograd_weights_host(wt, wm)
+    tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
+    work = torch.empty((wm + 2) ** 2 * tiles * (cin + cout), device=dev)
     got = torch.zeros(m * 80, device=dev)
-    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(got, 8, 80), wino=(T(ops.split_bf16x3_host(u), dev), work),
-               **kw)
+    ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(got, 8, 80),
+               wino=(T(ops.split_bf16x3_host(u), dev), work, wm), **kw)
     g, r = got.cpu().numpy().reshape(m, 80), ref.cpu().numpy().reshape(m, 80)
     np.testing.assert_allclose(g[:, 8:8 + cout], r[:, 8:8 + cout], rtol=2e-5, atol=2e-5)
     assert np.all(g[:, :8] == 0) and np.all(g[:, 8 + cout:] == 0)
     # bf16 planes: fp32 transforms, bf16-rounded V and U, fp32 accumulate
     got16 = torch.zeros(m * 80, device=dev)
     ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(got16, 8, 80),
-               wino=(T(ops.bf16_bits(u).reshape(1, -1).view(np.int16), dev), work))
+               wino=(T(ops.bf16_bits(u).reshape(1, -1).view(np.int16), dev), work, wm))
     plain = torch.zeros(m * cout, device=dev)
     ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(plain, 0, cout))
     d16 = got16.cpu().numpy().reshape(m, 80)[:, 8:8 + cout] - plain.cpu().numpy().reshape(m, cout)

@@ -84,15 +84,19 @@ def run_case(preset, tag=None, precision="fp32", model=None):
     return model
 
 
-def run_tiled_batch(preset, reps, precision):
+def run_tiled_batch(preset, reps, precision, **engine_kw):
     """The golden images tiled `reps` times into ONE batch through the drop-in model (eager, the engine's
     default micro-batch split: the path bench.py times) → (model, golden, post-processed dets, logits,
-    boxes, topk)."""
+    boxes, topk). engine_kw: Engine options other than the product defaults (e.g. wino_m=2)."""
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
     from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
 
     g = np.load(os.path.join(GOLD, f"{preset}_640.npz"))
     model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False, precision=precision)
+    if engine_kw:
+        model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision,
+                               **engine_kw)
     proc = SpotterImageProcessor()
     imgs = load_images(g) * reps
     n = len(imgs)
@@ -110,6 +114,14 @@ def run_tiled_batch(preset, reps, precision):
         topk = np.concatenate([eng._ctx(i)["ws"]["topk"][:(bounds[i + 1] - bounds[i]) * 300].cpu().numpy()
                                for i in range(mb)]).reshape(n, 300)
     return model, g, dets, out.logits.cpu().numpy(), out.pred_boxes.cpu().numpy(), topk
+
+
+def test_r101vd_bs32_winograd_f23_matches_hf_goldens():
+    """The headline batch with the F(2x2,3x3) Winograd variant (Engine(wino_m=2)) instead of the default
+    F(4x4,3x3): the same parity bar per image."""
+    model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, "fp32", wino_m=2)
+    for b in range(32):
+        check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b])
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])

@@ -225,29 +225,31 @@ def test_local_checkpoint_round_trip(tmp_path):
     assert all(np.array_equal(w2[k], w[k]) for k in w)
 
 
-def test_winograd_weight_transform_reproduces_the_direct_conv():
-    """ops.winograd_weights_host (U = G g Gᵀ, fp64 on the host) composed with the F(2x2,3x3) input /
-    output transforms the kernels apply (Bᵀ d B, Aᵀ M A; winograd.hip) is the 3x3 stride-1 pad-1
-    cross-correlation: checked in fp64 on a ragged map (odd H, W) against a direct conv."""
+@pytest.mark.parametrize("wm", [2, 4])
+def test_winograd_weight_transform_reproduces_the_direct_conv(wm):
+    """ops.winograd_weights_host (U = G g Gᵀ, fp64 on the host) composed with the F(m×m,3x3) input /
+    output transforms the kernels apply (Bᵀ d B, Aᵀ M A with ops.WINO_BT / WINO_AT, the constants of
+    winograd.hip) is the 3x3 stride-1 pad-1 cross-correlation: checked in fp64 on a ragged map (H, W not
+    multiples of the tile) against a direct conv."""
     from spotter_amd import ops
 
     rng = np.random.default_rng(3)
     n, h, w, ci, co = 2, 5, 7, 6, 4
+    a = wm + 2
     x = rng.standard_normal((n, h, w, ci))
     g = rng.standard_normal((co, 3, 3, ci)).astype(np.float32)
-    u = ops.winograd_weights_host(g).astype(np.float64).reshape(4, 4, co, ci)
-    bt = np.array([[1, 0, -1, 0], [0, 1, 1, 0], [0, -1, 1, 0], [0, 1, 0, -1]], np.float64)
-    at = np.array([[1, 1, 1, 0], [0, 1, -1, -1]], np.float64)
-    th, tw = (h + 1) // 2, (w + 1) // 2
-    xp = np.zeros((n, 2 * th + 2, 2 * tw + 2, ci))
+    u = ops.winograd_weights_host(g, wm).astype(np.float64).reshape(a, a, co, ci)
+    bt, at = ops.WINO_BT[wm], ops.WINO_AT[wm]
+    th, tw = (h + wm - 1) // wm, (w + wm - 1) // wm
+    xp = np.zeros((n, wm * th + 2, wm * tw + 2, ci))
     xp[:, 1:h + 1, 1:w + 1] = x
-    y = np.zeros((n, 2 * th, 2 * tw, co))
+    y = np.zeros((n, wm * th, wm * tw, co))
     for ty in range(th):
         for tx in range(tw):
-            d = xp[:, 2 * ty:2 * ty + 4, 2 * tx:2 * tx + 4]            # [n, 4, 4, ci]
+            d = xp[:, wm * ty:wm * ty + a, wm * tx:wm * tx + a]            # [n, a, a, ci]
             v = np.einsum("ai,nijc,bj->nabc", bt, d, bt)
             m = np.einsum("nabc,aboc->nabo", v, u)
-            y[:, 2 * ty:2 * ty + 2, 2 * tx:2 * tx + 2] = np.einsum("pa,nabo,qb->npqo", at, m, at)
+            y[:, wm * ty:wm * ty + wm, wm * tx:wm * tx + wm] = np.einsum("pa,nabo,qb->npqo", at, m, at)
     ref = np.zeros((n, h, w, co))
     xq = np.pad(x, ((0, 0), (1, 1), (1, 1), (0, 0)))
     for i in range(3):

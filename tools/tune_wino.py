@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--planes", type=int, default=3, choices=[1, 3])
     ap.add_argument("--shapes", default=None, help="n,h,w,cin,cout;... (default: the C2 shapes)")
     ap.add_argument("--cfgs", default=None)
+    ap.add_argument("--m", type=int, default=2, choices=[2, 4], help="Winograd output tile F(m×m, 3×3)")
     a = ap.parse_args()
     shapes = [tuple(int(v) for v in s.split(",")) for s in a.shapes.split(";")] if a.shapes else SHAPES
     cfgs = a.cfgs.split(",") if a.cfgs else CFGS
@@ -61,7 +62,7 @@ def main():
         x = torch.randn(n * h * w * cin, device=dev, generator=g)
         wt_host = (np.random.default_rng(0).standard_normal((cout, 3, 3, cin)) / np.sqrt(9 * cin)).astype(np.float32)
         wt = torch.from_numpy(wt_host.reshape(cout, -1)).to(dev)
-        u = ops.winograd_weights_host(wt_host)
+        u = ops.winograd_weights_host(wt_host, a.m)
         if a.planes == 3:
             direct_kw = {"wt_planes": ops.split_bf16x3(wt)}
             planes = torch.from_numpy(ops.split_bf16x3_host(u)).to(dev)
@@ -69,8 +70,8 @@ def main():
             direct_kw = {"wt16": torch.from_numpy(ops.bf16_bits(wt_host.reshape(cout, -1)).view(np.int16)).to(dev)}
             planes = torch.from_numpy(ops.bf16_bits(u).reshape(1, -1).view(np.int16)).to(dev)
         out = torch.empty(n * h * w * cout, device=dev)
-        tiles = n * ((h + 1) // 2) * ((w + 1) // 2)
-        work = torch.empty(16 * tiles * (cin + cout), device=dev)
+        tiles = n * ((h + a.m - 1) // a.m) * ((w + a.m - 1) // a.m)
+        work = torch.empty((a.m + 2) ** 2 * tiles * (cin + cout), device=dev)
         ws = torch.empty(16 << 20, device=dev)
         sh = torch.zeros(cout, device=dev)
         direct = timeit(lambda: ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, 3, 1, 1, view(out, cout), shift=sh,
@@ -81,7 +82,7 @@ def main():
             try:
                 times[cfg] = round(timeit(lambda: ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, 3, 1, 1,
                                                              view(out, cout), shift=sh, act="silu",
-                                                             wino=(planes, work)), a.reps), 4)
+                                                             wino=(planes, work, a.m)), a.reps), 4)
             except RuntimeError:
                 pass
             finally:
@@ -103,7 +104,7 @@ def main():
         try:
             for _ in range(a.reps):
                 ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, 3, 1, 1, view(out, cout), shift=sh, act="silu",
-                           wino=(planes, work))
+                           wino=(planes, work, a.m))
             torch.cuda.synchronize()
         finally:
             ops.set_launch_hook(None)
@@ -112,7 +113,7 @@ def main():
         for key, recs in stages.items():
             ms = sum(e0.elapsed_time(e1) for e0, e1, _ in recs) / len(recs)
             split[key] = {"ms": round(ms, 4), "GB/s": round(recs[0][2] / (ms * 1e-3) / 1e9, 1)}
-        e = {"shape": [n, h, w, cin, cout], "planes": a.planes, "direct_ms": round(direct, 4), "best_cfg": best,
+        e = {"shape": [n, h, w, cin, cout], "m": a.m, "planes": a.planes, "direct_ms": round(direct, 4), "best_cfg": best,
              "best_ms": times[best], "speedup": round(direct / times[best], 3), "stages": split, "times": times}
         res.append(e)
         print(json.dumps(e), flush=True)
