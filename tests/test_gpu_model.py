@@ -262,6 +262,25 @@ def test_graph_replay_matches_eager():
         assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)
 
 
+def test_graph_replay_bs4_with_winograd():
+    """bs4 (the largest graph-replayed batch) runs the Winograd 3x3s (>= 8192 output pixels: the RepVGG
+    convs and the 80² / 40² backbone conv2s) inside the captured graph: replay equals eager bit for bit."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+    from spotter_amd.synthetic import synthetic_image
+
+    model = SpotterForObjectDetection(PRESETS["r18vd"], use_graphs=True)
+    proc = SpotterImageProcessor()
+    x = proc(images=[synthetic_image(s) for s in (11, 12, 13, 14)])["pixel_values"]
+    e = model(pixel_values=x)          # eager (first sight of the shape)
+    eng = model.engine
+    assert any(cw.wino is not None for cs in eng.fpn + eng.pan for _, cw in cs["reps"])
+    g1 = model(pixel_values=x)         # captures + replays
+    g2 = model(pixel_values=x)         # replay
+    for o in (g1, g2):
+        assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)
+
+
 def test_bf16_variant_close_to_fp32_goldens():
     """bf16 MFMA variant (reported separately): detections stay close to the fp32 reference.
     The flat-gray golden has 300 same-label detections on overlapping boxes, where IoU matching
