@@ -258,6 +258,19 @@ def test_winograd_weight_transform_reproduces_the_direct_conv(wm):
     np.testing.assert_allclose(y[:, :h, :w], ref, rtol=1e-6, atol=1e-5)
 
 
+def test_winograd_kernel_constants_match_host_matrices():
+    """The Bᵀ / Aᵀ constants compiled into winograd.hip (kBT43, kAT43) are the matrices the host-side
+    weight transform and the CPU reproduction test use (ops.WINO_BT / WINO_AT), entry for entry."""
+    from spotter_amd import ops
+
+    src = open(os.path.join(os.path.dirname(__file__), "..", "spotter_amd", "csrc", "winograd.hip")).read()
+    for name, ref in (("kBT43", ops.WINO_BT[4]), ("kAT43", ops.WINO_AT[4])):
+        body = src[src.index(f"constexpr float {name}"):]
+        body = body[body.index("{"):body.index("};")]
+        vals = [float(v.rstrip("f")) for v in re.findall(r"-?\d+\.\d*f?", body)]
+        assert np.array_equal(np.array(vals).reshape(ref.shape), ref), name
+
+
 def test_weight_split_on_host_matches_torch_rne():
     """ops.split_bf16x3_host / bf16_bits (numpy, pack time) against torch's own RNE bf16 cast on the CPU:
     hi / mid / lo bit-identical to the chained casts, and hi + mid + lo == w exactly."""
