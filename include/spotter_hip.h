@@ -160,8 +160,8 @@ int sp_winograd_f23_output(const sp_conv_desc* d, const float* work, int64_t wor
 /* The same three stages for F(4x4, 3x3) (ABI v9): 4x4 output tiles, T = N * ceil(H/4) * ceil(W/4), 36
  * components (component ab = 6a + b), interpolation points (0, -1, 1, 1/2, -2, inf); wt_wino
  * [planes][36][Cout][Cin] (U = G g G^T in fp64 on the host), work >= 36 * T * (Cin + Cout) elements.
- * 1/4 of the direct conv's multiply-adds; fp32 error 3-5x the direct conv's (within the split
- * kernel's fp32-accuracy bar, tests/test_gpu_kernels.py::test_winograd_*). */
+ * 1/4 of the direct conv's multiply-adds; fp32 error 3-5x the direct conv's, under 1e-5 of the output
+ * scale (tests/test_gpu_kernels.py::test_winograd_is_fp32_accurate). */
 int sp_winograd_f43_input(const sp_conv_desc* d, float* work, int64_t work_elems, void* stream);
 int sp_winograd_f43_gemm(const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride, float* work,
                          int64_t work_elems, void* stream);

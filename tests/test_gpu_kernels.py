@@ -31,6 +31,14 @@ def _reset_conv_config():
     ops.force_conv_config(None)
 
 
+def seed(case, k=0):
+    """A per-case RNG seed that does not depend on PYTHONHASHSEED (hash() of a tuple holding strings is
+    randomised per process, which would make the fp32-accuracy cases draw new data every run)."""
+    import zlib
+
+    return zlib.crc32(repr(case).encode()) + k
+
+
 def T(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
@@ -77,7 +85,7 @@ def test_conv2d_matches_oracle(dev, case, workspace=None):
     from spotter_amd.ops import view
 
     n, h, w, cin, cout, k, st, act = case
-    rng = np.random.default_rng(hash(case) % 2**32)
+    rng = np.random.default_rng(seed(case))
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
     wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
     sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
@@ -138,7 +146,7 @@ def test_conv2d_bf16_matches_bf16_rounded_reference(dev, case, cfg, monkeypatch)
     if cfg:
         ops.force_conv_config(cfg)
     n, h, w, cin, cout, k, st, act = case
-    rng = np.random.default_rng(hash(case) % 2**32 + 1)
+    rng = np.random.default_rng(seed(case, 1))
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
     wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
     sc = rng.uniform(0.5, 1.5, cout).astype(np.float32)
@@ -181,7 +189,7 @@ def test_conv2d_f32x3_is_fp32_accurate(dev, case, cfg, monkeypatch):
     from spotter_amd.ops import view
 
     n, h, w, cin, cout, k, st, _ = case
-    rng = np.random.default_rng(hash(case) % 2**32 + 2)
+    rng = np.random.default_rng(seed(case, 2))
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
     wt = (rng.standard_normal((cout, cin, k, k)) / np.sqrt(cin * k * k)).astype(np.float32)
     pad = k // 2
@@ -222,13 +230,15 @@ WINO_CFGS = [None, "63", "33", "14", "45"]
 @pytest.mark.parametrize("wm", [2, 4])
 def test_winograd_is_fp32_accurate(dev, case, cfg, wm):
     """sp_winograd_f{2,4}3_* (F(m×m,3x3): fp32 transforms + the split GEMM) against an fp64 conv of the
-    same fp32 operands: within 2x the fp32 MFMA direct conv's max error (+1e-6 of the output scale) and
-    under 1e-5 of the output scale — the bar of test_conv2d_f32x3_is_fp32_accurate."""
+    same fp32 operands, under 1e-5 of the output scale outright (the bar of
+    test_conv2d_f32x3_is_fp32_accurate) and against the fp32 MFMA direct conv's own max error e32:
+    F(2×2) within 2·e32 (+1e-6 of the scale), F(4×4) within 5·e32 — its documented error is 3-5× the
+    direct conv's (tools/wino_error_study.py)."""
     from spotter_amd import ops
     from spotter_amd.ops import view
 
     n, h, w, cin, cout, _ = case
-    rng = np.random.default_rng(hash(case) % 2**32 + 5)
+    rng = np.random.default_rng(seed(case, 5))
     x = rng.standard_normal((n, h, w, cin)).astype(np.float32)
     wt = (rng.standard_normal((cout, cin, 3, 3)) / np.sqrt(cin * 9)).astype(np.float32)
     ref = _conv64(x, wt, 1, 1)
@@ -250,7 +260,7 @@ def test_winograd_is_fp32_accurate(dev, case, cfg, wm):
     ew = np.abs(got - ref).max()
     scale = np.abs(ref).max()
     assert np.isfinite(got).all()
-    assert ew <= 2 * e32 + 1e-6 * scale, (ew, e32, scale)
+    assert ew <= (2 if wm == 2 else 5) * e32 + 1e-6 * scale, (ew, e32, scale)
     assert ew <= 1e-5 * scale, (ew, scale)
 
 
