@@ -16,6 +16,7 @@
 // consecutive threads on consecutive 4-channel groups: the input transform takes two adjacent tiles
 // per thread (24 float4 loads, 32 float4 stores), the output transform one tile (16 non-temporal
 // float4 loads, 4 float4 stores + the epilogue's residual loads).
+#include <cstdlib>
 #include "conv_common.h"
 
 namespace sp {
@@ -140,8 +141,7 @@ __global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restri
 // 4t-1 .. 4t+4), 36 components, 36/(16·9) = 1/4 of the direct conv's multiply-adds. The points are
 // chosen for fp32 error (numpy study, DESIGN §4: max |e| / Σ|ab| 3.6e-7 vs 1.0e-6 for the common
 // (0, ±1, ±2) set and 7.7e-8 for the direct conv); Bᵀ and Aᵀ hold small dyadic values (exact in fp32),
-// G (thirds, fifteenths) is applied in fp64 on the host. Two channels per thread keep the 6×6 partial
-// sums in ~100 VGPRs.
+// G (thirds, fifteenths) is applied in fp64 on the host.
 constexpr float kBT43[6][6] = {{1.f, -1.5f, -2.f, 1.5f, 1.f, 0.f},  {0.f, 1.f, -2.5f, 0.5f, 1.f, 0.f},
                                {0.f, -1.f, 0.5f, 2.5f, 1.f, 0.f},   {0.f, -2.f, -1.f, 2.f, 1.f, 0.f},
                                {0.f, 0.5f, -1.f, -0.5f, 1.f, 0.f},  {0.f, 1.f, -1.5f, -2.f, 1.5f, 1.f}};
@@ -150,40 +150,46 @@ constexpr float kAT43[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
                                {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
                                {0.f, -1.f, 1.f, 0.125f, -8.f, 1.f}};
 
+template <int VW>
+struct VT {
+  typedef float type __attribute__((ext_vector_type(VW)));
+};
+
+// VW consecutive channels per thread (1 or 2: the launch takes 1 on maps too small to fill the chip
+// with 2-channel threads).
+template <int VW>
 __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
-                                                          int c2n, int th, int tw, int64_t T,
+                                                          int cvn, int th, int tw, int64_t T,
                                                           float* __restrict__ V, int64_t cin) {
-  const int64_t total = T * c2n;
+  typedef typename VT<VW>::type vf;
+  const int64_t total = T * cvn;
   const int64_t plane = T * cin;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = g / c2n;
-    const int c = (int)(g - t * c2n) * 2;
+    const int64_t t = g / cvn;
+    const int c = (int)(g - t * cvn) * VW;
     const int64_t b = t / ((int64_t)th * tw);
     const int r = (int)(t - b * th * tw);
     const int ty = r / tw;
     const int tx = r - ty * tw;
     const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
-    float2 q[6][6];  // row pass: q[i][bb] = Σ_j Bᵀ[bb][j] d[i][j]
+    vf q[6][6];  // row pass: q[i][bb] = Σ_j Bᵀ[bb][j] d[i][j]
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      float2 dr[6];
+      vf dr[6];
       const int yy = y0 + i;
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int xx = x0 + j;
         dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-                    ? *reinterpret_cast<const float2*>(x + ((b * h + yy) * w + xx) * lda + c)
-                    : make_float2(0.f, 0.f);
+                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
+                    : vf(0.f);
       }
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) {
-        float2 acc = make_float2(0.f, 0.f);
+        vf acc = vf(0.f);
 #pragma unroll
         for (int j = 0; j < 6; ++j)
-          if (kBT43[bb][j] != 0.f) {
-            acc.x = fmaf(kBT43[bb][j], dr[j].x, acc.x);
-            acc.y = fmaf(kBT43[bb][j], dr[j].y, acc.y);
-          }
+          if (kBT43[bb][j] != 0.f) acc = __builtin_elementwise_fma(vf(kBT43[bb][j]), dr[j], acc);
         q[i][bb] = acc;
       }
     }
@@ -192,74 +198,49 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
     for (int bb = 0; bb < 6; ++bb)
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
-        float2 v = make_float2(0.f, 0.f);
+        vf v = vf(0.f);
 #pragma unroll
         for (int i = 0; i < 6; ++i)
-          if (kBT43[a][i] != 0.f) {
-            v.x = fmaf(kBT43[a][i], q[i][bb].x, v.x);
-            v.y = fmaf(kBT43[a][i], q[i][bb].y, v.y);
-          }
-        *reinterpret_cast<float2*>(dst + (a * 6 + bb) * plane) = v;
+          if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
+        *reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane) = v;
       }
   }
 }
 
-__device__ __forceinline__ float2 epi2(float2 v, const sp_conv_desc& d, int64_t m, int n) {
-  const float2 sc = d.scale ? *reinterpret_cast<const float2*>(d.scale + n) : make_float2(1.f, 1.f);
-  const float2 sh = d.shift ? *reinterpret_cast<const float2*>(d.shift + n) : make_float2(0.f, 0.f);
-  v.x = fmaf(v.x, sc.x, sh.x);
-  v.y = fmaf(v.y, sc.y, sh.y);
-  if (d.res1) {
-    const float2 a = *reinterpret_cast<const float2*>(d.res1 + m * d.ldr1 + n);
-    v.x += a.x;
-    v.y += a.y;
-  }
-  v.x = act_apply(v.x, d.act);
-  v.y = act_apply(v.y, d.act);
-  if (d.res2) {
-    const float2 a = *reinterpret_cast<const float2*>(d.res2 + m * d.ldr2 + n);
-    v.x += a.x;
-    v.y += a.y;
-  }
-  return v;
-}
-
-__global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restrict__ Mc, int64_t T, int c2n,
+template <int VW>
+__global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restrict__ Mc, int64_t T, int cvn,
                                                            int th, int tw, const sp_conv_desc d) {
-  const int64_t total = T * c2n;
+  typedef typename VT<VW>::type vf;
+  const int64_t total = T * cvn;
   const int64_t cout = d.Cout;
   const int64_t plane = T * cout;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = g / c2n;
-    const int n = (int)(g - t * c2n) * 2;
+    const int64_t t = g / cvn;
+    const int n = (int)(g - t * cvn) * VW;
     const int64_t b = t / ((int64_t)th * tw);
     const int r = (int)(t - b * th * tw);
     const int ty = r / tw;
     const int tx = r - ty * tw;
     const float* src = Mc + t * cout + n;
-    float2 s[4][6];  // s[p][bb] = Σ_a Aᵀ[p][a] M[a][bb], accumulated as the rows of M arrive
+    vf s[4][6];  // s[p][bb] = Σ_a Aᵀ[p][a] M[a][bb], accumulated as the rows of M arrive
 #pragma unroll
     for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int bb = 0; bb < 6; ++bb) s[p][bb] = make_float2(0.f, 0.f);
+      for (int bb = 0; bb < 6; ++bb) s[p][bb] = vf(0.f);
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
-      float2 mr[6];
+      vf mr[6];
 #pragma unroll
-      for (int bb = 0; bb < 6; ++bb) {
-        typedef float v2f __attribute__((ext_vector_type(2)));
-        const v2f v = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(src + (a * 6 + bb) * plane));
-        mr[bb] = make_float2(v.x, v.y);
-      }
+      for (int bb = 0; bb < 6; ++bb)
+        mr[bb] = __builtin_nontemporal_load(reinterpret_cast<const vf*>(src + (a * 6 + bb) * plane));
 #pragma unroll
       for (int p = 0; p < 4; ++p)
         if (kAT43[p][a] != 0.f)
 #pragma unroll
-          for (int bb = 0; bb < 6; ++bb) {
-            s[p][bb].x = fmaf(kAT43[p][a], mr[bb].x, s[p][bb].x);
-            s[p][bb].y = fmaf(kAT43[p][a], mr[bb].y, s[p][bb].y);
-          }
+          for (int bb = 0; bb < 6; ++bb) s[p][bb] = __builtin_elementwise_fma(vf(kAT43[p][a]), mr[bb], s[p][bb]);
     }
+    const vf sc = d.scale ? *reinterpret_cast<const vf*>(d.scale + n) : vf(1.f);
+    const vf sh = d.shift ? *reinterpret_cast<const vf*>(d.shift + n) : vf(0.f);
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int oy = 4 * ty + p;
@@ -268,18 +249,41 @@ __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restri
       for (int qq = 0; qq < 4; ++qq) {
         const int ox = 4 * tx + qq;
         if (ox >= d.Wo) break;
-        float2 y = make_float2(0.f, 0.f);
+        vf y = vf(0.f);
 #pragma unroll
         for (int bb = 0; bb < 6; ++bb)
-          if (kAT43[qq][bb] != 0.f) {
-            y.x = fmaf(kAT43[qq][bb], s[p][bb].x, y.x);
-            y.y = fmaf(kAT43[qq][bb], s[p][bb].y, y.y);
-          }
+          if (kAT43[qq][bb] != 0.f) y = __builtin_elementwise_fma(vf(kAT43[qq][bb]), s[p][bb], y);
         const int64_t m = (b * d.Ho + oy) * d.Wo + ox;
-        *reinterpret_cast<float2*>(d.C + m * d.ldc + n) = epi2(y, d, m, n);
+        y = __builtin_elementwise_fma(y, sc, sh);
+        if (d.res1) y += *reinterpret_cast<const vf*>(d.res1 + m * d.ldr1 + n);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) y[e] = act_apply(y[e], d.act);
+        if (d.res2) y += *reinterpret_cast<const vf*>(d.res2 + m * d.ldr2 + n);
+        *reinterpret_cast<vf*>(d.C + m * d.ldc + n) = y;
       }
     }
   }
+}
+
+// Channels per thread of the F(4×4) transforms (profiles/r2/wino43_vw_ab.json, same-box A/B): the
+// output transform is 2-10 % faster on one channel per thread at every C2 shape (more waves in flight
+// hide the strided M reads); the input transform gains from two on large maps and loses on small ones
+// (below 2^18 tile × channel items: bs1/bs8 maps). SP_WINO43_VW=1|2 in the environment forces one.
+int wino43_forced_vw() {
+  static const int forced = [] {
+    const char* e = getenv("SP_WINO43_VW");
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 2 ? v : 0;
+  }();
+  return forced;
+}
+int wino43_in_vw(int64_t items) {
+  const int f = wino43_forced_vw();
+  return f ? f : items < (int64_t(1) << 18) ? 1 : 2;
+}
+int wino43_out_vw() {
+  const int f = wino43_forced_vw();
+  return f ? f : 1;
 }
 
 int stream_grid(int64_t work) {
@@ -345,9 +349,12 @@ int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t wor
     hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream),
                        d->A, d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
   } else {
-    const int cin2 = d->Cin / 2;
-    hipLaunchKernelGGL(wino_in_f43_kernel, dim3(stream_grid(T * cin2)), dim3(256), 0, as_stream(stream), d->A,
-                       d->lda, d->H, d->W, cin2, th, tw, T, work, (int64_t)d->Cin);
+    if (wino43_in_vw(T * d->Cin) == 1)
+      hipLaunchKernelGGL(wino_in_f43_kernel<1>, dim3(stream_grid(T * d->Cin)), dim3(256), 0, as_stream(stream),
+                         d->A, d->lda, d->H, d->W, d->Cin, th, tw, T, work, (int64_t)d->Cin);
+    else
+      hipLaunchKernelGGL(wino_in_f43_kernel<2>, dim3(stream_grid(T * d->Cin / 2)), dim3(256), 0, as_stream(stream),
+                         d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T, work, (int64_t)d->Cin);
   }
   return check_launch(what);
 }
@@ -422,9 +429,12 @@ int wino_output(const char* what, const sp_conv_desc* d, const float* work, int6
     hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
                        work + NC * T * d->Cin, T, cout4, th, tw, *d);
   } else {
-    const int cout2 = d->Cout / 2;
-    hipLaunchKernelGGL(wino_out_f43_kernel, dim3(stream_grid(T * cout2)), dim3(256), 0, as_stream(stream),
-                       work + NC * T * d->Cin, T, cout2, th, tw, *d);
+    if (wino43_out_vw() == 1)
+      hipLaunchKernelGGL(wino_out_f43_kernel<1>, dim3(stream_grid(T * d->Cout)), dim3(256), 0, as_stream(stream),
+                         work + NC * T * d->Cin, T, d->Cout, th, tw, *d);
+    else
+      hipLaunchKernelGGL(wino_out_f43_kernel<2>, dim3(stream_grid(T * d->Cout / 2)), dim3(256), 0,
+                         as_stream(stream), work + NC * T * d->Cin, T, d->Cout / 2, th, tw, *d);
   }
   return check_launch(what);
 }
