@@ -22,6 +22,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=fast",
          "-Xarch_host", "-ffp-contract=off", "-munsafe-fp-atomics", f"-I{INCLUDE}"]
+# SP_TUNING_BUILD=1 compiles the tuning-only environment overrides in (e.g. SP_WINO43_VW in winograd.hip);
+# the product library reads no environment. Rebuild with --force when toggling it.
+if os.environ.get("SP_TUNING_BUILD") == "1":
+    FLAGS.append("-DSP_TUNING_BUILD")
 
 
 def sources():

@@ -268,14 +268,20 @@ __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restri
 // Channels per thread of the F(4×4) transforms (profiles/r2/wino43_vw_ab.json, same-box A/B): the
 // output transform is 2-10 % faster on one channel per thread at every C2 shape (more waves in flight
 // hide the strided M reads); the input transform gains from two on large maps and loses on small ones
-// (below 2^18 tile × channel items: bs1/bs8 maps). SP_WINO43_VW=1|2 in the environment forces one.
+// (below 2^18 tile × channel items: bs1/bs8 maps). The results are the same either way (per-channel
+// arithmetic is identical). A tuning build (-DSP_TUNING_BUILD) lets SP_WINO43_VW=1|2 force one for such
+// A/Bs; the product build reads no environment.
 int wino43_forced_vw() {
+#ifdef SP_TUNING_BUILD
   static const int forced = [] {
     const char* e = getenv("SP_WINO43_VW");
     const int v = e ? atoi(e) : 0;
     return v == 1 || v == 2 ? v : 0;
   }();
   return forced;
+#else
+  return 0;
+#endif
 }
 int wino43_in_vw(int64_t items) {
   const int f = wino43_forced_vw();

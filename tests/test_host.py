@@ -54,6 +54,17 @@ def test_library_exports_every_header_symbol():
     assert L.sp_abi_version() == _lib.ABI_VERSION
 
 
+def test_product_library_reads_no_environment():
+    """Tile / transform choices come from the ABI (sp_set_conv_config) and the compiled tables only: the
+    environment overrides of the tuning tools exist only in an SP_TUNING_BUILD=1 library."""
+    from spotter_amd.build_ext import LIB, build
+
+    if not os.path.exists(LIB):
+        build(verbose=False)
+    out = subprocess.run(["nm", "-D", "--undefined-only", LIB], capture_output=True, text=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", out), "libspotter_hip.so imports getenv"
+
+
 def test_arg_errors_are_reported_without_a_gpu():
     """Argument validation runs on the host and returns <0 with a message (no device touched)."""
     import ctypes as C
