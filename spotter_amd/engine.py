@@ -409,13 +409,21 @@ class Engine:
     # ------------------------------------------------------------------ layers
     SPLITK_ELEMS = 16 << 20  # 64 MB fp32 split-K scratch per context
     WINO_MIN_PIXELS = 8192
+    WINO43_MIN_WORK = 1 << 19
+
+    def _wino_pays(self, pixels: int, cin: int) -> bool:
+        """Size gate of the Winograd path. F(2x2): maps of >= 8192 output pixels (2048 tiles): at bs1 the
+        40² / 20² convs measured 0.69-1.07x of the split-K implicit GEMM, from bs8 up 1.2-1.8x
+        (profiles/r2/tune_wino_x3_bs8_bs1.json). F(4x4): pixels x Cin >= 2^19: at bs1 the 80²x384 /
+        40²x384 / 80²x128 convs measured 2.6x / 1.45x / 1.09x, 40²x256 1.04x, 20²x384 / 20²x512 0.85-0.95x
+        (profiles/r2/tune_wino_f43_bs1.json); every bs8 / bs32 map clears it."""
+        if self.wino_m == 4:
+            return pixels * cin >= self.WINO43_MIN_WORK
+        return pixels >= self.WINO_MIN_PIXELS
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        # Winograd only on maps of >= 8192 output pixels (2048 2x2 tiles): at bs1 the 40² / 20² convs
-        # measured 0.69-1.07x of the split-K implicit GEMM (profiles/r2/tune_wino_x3_bs8_bs1.json), from
-        # bs8 up 1.2-1.8x
-        if cw.wino is not None and stride == 1 and not kw and n * h * w >= self.WINO_MIN_PIXELS:
+        if cw.wino is not None and stride == 1 and not kw and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
             work = self._buf("wino_work", (wm + 2) ** 2 * tiles * (cw.cin + cw.cout))

@@ -281,6 +281,33 @@ def test_graph_replay_bs4_with_winograd():
         assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)
 
 
+def test_graph_replay_bs1_runs_winograd_f43():
+    """bs1 (the /detect latency path): the F(4x4) size gate (pixels x Cin >= 2^19) sends the 80² / 40²
+    encoder RepVGG convs through Winograd; eager runs the transform kernels, graph replay equals eager."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor, ops
+    from spotter_amd.config import PRESETS
+    from spotter_amd.synthetic import synthetic_image
+
+    model = SpotterForObjectDetection(PRESETS["r101vd"], use_graphs=True)
+    x = SpotterImageProcessor()(images=synthetic_image(21))["pixel_values"]
+    kinds = []
+
+    def hook(kind, launch, flops, nbytes, shape=None):
+        kinds.append(kind)
+        launch()
+
+    ops.set_launch_hook(hook)
+    try:
+        e = model(pixel_values=x)      # eager (first sight of the shape)
+    finally:
+        ops.set_launch_hook(None)
+    assert kinds.count("wino_tf") >= 2 * 9, kinds.count("wino_tf")  # 3 RepVGG convs per CSPRep block x 3+
+    g1 = model(pixel_values=x)         # captures + replays
+    g2 = model(pixel_values=x)         # replay
+    for o in (g1, g2):
+        assert torch.equal(o.logits, e.logits) and torch.equal(o.pred_boxes, e.pred_boxes)
+
+
 def test_bf16_variant_close_to_fp32_goldens():
     """bf16 MFMA variant (reported separately): detections stay close to the fp32 reference.
     The flat-gray golden has 300 same-label detections on overlapping boxes, where IoU matching
