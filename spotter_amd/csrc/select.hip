@@ -9,8 +9,8 @@
 // One 1024-thread workgroup per row: keys (order-preserving uint32 of the
 // fp32 value, after the optional max-over-C reduction / sigmoid) live in LDS
 // (≤ 36,864 per row); four 8-bit radix passes find the k-th largest key T;
-// keys > T are compacted, keys == T are taken in index order; a bitonic sort on
-// (key desc, index asc) orders the k winners. Deterministic.
+// keys > T are compacted, keys == T are taken in index order; each winner's rank
+// under (key desc, index asc) places it. Deterministic.
 #include "common.h"
 
 namespace sp {
@@ -103,26 +103,47 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     for (int i = tid; i < kHist * 256; i += kThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
     const uint32_t prefix = s_sel[0];
+    const uint32_t rem = s_sel[1];  // read before the selecting thread rewrites it below
+    // keys that survived the earlier digits crowd into a few bins (sigmoid scores share their top bytes),
+    // so each wave adds its most common case — the lanes matching the first live lane's digit — with one
+    // atomic, and only the other lanes add their own
     for (int i = tid; i < n; i += kThreads) {
       const uint32_t key = keys[i];
-      if ((key & mask) == prefix) atomicAdd(&my_hist[(key >> shift) & 255u], 1u);
+      const bool live = (key & mask) == prefix;
+      const uint32_t dg = (key >> shift) & 255u;
+      const unsigned long long act = __ballot(live);
+      if (act) {
+        const int lead = __ffsll((long long)act) - 1;
+        const uint32_t ld = __shfl(dg, lead);
+        const bool same = live && dg == ld;
+        const unsigned long long sm = __ballot(same);
+        if (live && !same) atomicAdd(&my_hist[dg], 1u);
+        if ((tid & 63) == lead) atomicAdd(&my_hist[ld], (uint32_t)__popcll(sm));
+      }
+    }
+    __syncthreads();
+    // the digit of the k-th largest key: bin b with above(b) < rem <= above(b) + hist(b), where above(b)
+    // = Σ hist over bins > b — a suffix scan over the 256 bins in four waves (shuffles + 4 wave totals)
+    // instead of one thread walking the bins
+    uint32_t tot = 0, suf = 0;
+    if (tid < 256) {
+      for (int j = 0; j < kHist; ++j) tot += hist[j][tid];
+      suf = tot;  // becomes Σ hist over bins >= tid within this wave
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_down(suf, off);
+        if ((tid & 63) + off < 64) suf += t;
+      }
+      if ((tid & 63) == 0) wave_tot[tid >> 6] = suf;
     }
     __syncthreads();
     if (tid < 256) {
-      uint32_t tot = 0;
-      for (int j = 0; j < kHist; ++j) tot += hist[j][tid];
-      hist[0][tid] = tot;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t rem = s_sel[1], cum = 0;
-      int bsel = 0;
-      for (int bin = 255; bin >= 0; --bin) {
-        if (cum + hist[0][bin] >= rem) { bsel = bin; break; }
-        cum += hist[0][bin];
+      for (int w = (tid >> 6) + 1; w < 4; ++w) suf += wave_tot[w];
+      const uint32_t above = suf - tot;
+      if (above < rem && rem <= suf) {
+        s_sel[0] = prefix | ((uint32_t)tid << shift);
+        s_sel[1] = rem - above;
       }
-      s_sel[0] = prefix | ((uint32_t)bsel << shift);
-      s_sel[1] = rem - cum;
     }
     mask |= 255u << shift;
     __syncthreads();
@@ -130,55 +151,59 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
   const uint32_t T = s_sel[0];
   const uint32_t need_eq = s_sel[1];
   const uint32_t n_gt = (uint32_t)k - need_eq;
-  // keys > T: any order (sorted below)
+  // keys > T: any order (ranked below); count the keys == T alongside
   for (int i = tid; i < n; i += kThreads) {
     const uint32_t key = keys[i];
     if (key > T) {
-      uint32_t pos = atomicAdd(&s_sel[2], 1u);
+      const uint32_t pos = atomicAdd(&s_sel[2], 1u);
       cand[pos] = ((unsigned long long)key << 32) | (0xffffffffu - (uint32_t)i);
+    } else if (key == T) {
+      atomicAdd(&s_sel[3], 1u);
     }
-  }
-  // keys == T: the first need_eq in index order (ordered block compaction)
-  const int lane = tid & 63, wid = tid >> 6;
-  uint32_t taken = 0;
-  for (int base = 0; base < n && taken < need_eq; base += kThreads) {
-    const int i = base + tid;
-    const bool f = i < n && keys[i] == T;
-    const unsigned long long bal = __ballot(f);
-    const uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_tot[wid] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (int w = 0; w < kThreads / 64; ++w) {
-      if (w < wid) off += wave_tot[w];
-      tot += wave_tot[w];
-    }
-    const uint32_t pos = taken + off + before;
-    if (f && pos < need_eq)
-      cand[n_gt + pos] = ((unsigned long long)T << 32) | (0xffffffffu - (uint32_t)i);
-    taken += tot;
-    __syncthreads();
   }
   __syncthreads();
-  // bitonic sort of kMaxK entries, descending
-  for (int size = 2; size <= kMaxK; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = tid; t < kMaxK / 2; t += kThreads) {
-        const int lo = 2 * stride * (t / stride) + (t % stride);
-        const int hi = lo + stride;
-        const bool desc = ((lo & size) == 0);
-        unsigned long long a = cand[lo], b = cand[hi];
-        if ((a < b) == desc) { cand[lo] = b; cand[hi] = a; }
+  if (s_sel[3] == need_eq) {
+    // every key == T is taken (no tie across the cut): append them in any order after the n_gt above
+    for (int i = tid; i < n; i += kThreads)
+      if (keys[i] == T) {
+        const uint32_t pos = atomicAdd(&s_sel[2], 1u);
+        cand[pos] = ((unsigned long long)T << 32) | (0xffffffffu - (uint32_t)i);
       }
+  } else {
+    // a tie across the cut: the first need_eq keys == T in index order (ordered block compaction)
+    const int lane = tid & 63, wid = tid >> 6;
+    uint32_t taken = 0;
+    for (int base = 0; base < n && taken < need_eq; base += kThreads) {
+      const int i = base + tid;
+      const bool f = i < n && keys[i] == T;
+      const unsigned long long bal = __ballot(f);
+      const uint32_t before = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+      if (lane == 0) wave_tot[wid] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t off = 0, tot = 0;
+      for (int w = 0; w < kThreads / 64; ++w) {
+        if (w < wid) off += wave_tot[w];
+        tot += wave_tot[w];
+      }
+      const uint32_t pos = taken + off + before;
+      if (f && pos < need_eq)
+        cand[n_gt + pos] = ((unsigned long long)T << 32) | (0xffffffffu - (uint32_t)i);
+      taken += tot;
       __syncthreads();
     }
   }
+  __syncthreads();
+  // order the k winners by (key desc, index asc): every entry is distinct (the index is in the low word),
+  // so its position is the number of entries greater than it — one pass of broadcast LDS reads per
+  // thread, no sorting network
   for (int i = tid; i < k; i += kThreads) {
     const unsigned long long e = cand[i];
+    int rank = 0;
+    for (int j = 0; j < k; ++j) rank += cand[j] > e;
     const uint32_t key = (uint32_t)(e >> 32);
     const uint32_t id = 0xffffffffu - (uint32_t)(e & 0xffffffffu);
-    idx_out[row * k + i] = (int32_t)id;
-    if (vals) vals[row * k + i] = key2f(key);
+    idx_out[row * k + rank] = (int32_t)id;
+    if (vals) vals[row * k + rank] = key2f(key);
   }
 }
 

@@ -533,7 +533,9 @@ def test_msda_matches_oracle(dev, pad):
 
 
 @pytest.mark.parametrize("n,k,reduce_c,ties", [(8400, 300, 1, False), (1000, 300, 80, False),
-                                               (24000, 300, 1, False), (5000, 300, 1, True), (300, 300, 1, True)])
+                                               (24000, 300, 1, False), (5000, 300, 1, True), (300, 300, 1, True),
+                                               (36864, 512, 1, True), (36864, 512, 1, False), (33600, 300, 1, False),
+                                               (10, 1, 1, False), (700, 1, 1, True), (4096, 257, 4, True)])
 def test_topk_exact(dev, n, k, reduce_c, ties):
     from spotter_amd import ops
     from spotter_amd.ops import V
