@@ -28,6 +28,8 @@ class MicroBatcher:
         self.max_batch = max_batch
         self.max_wait = max_wait_ms / 1e3
         self._q: queue.Queue = queue.Queue()
+        self._pending = 0  # submitted, not yet resolved: nobody beyond the taken ones → no wait
+        self._pending_lock = threading.Lock()
         self.batches = 0  # engine forwards run (diagnostics / tests)
         self.images = 0
         self._thread = threading.Thread(target=self._loop, name="spotter-microbatcher", daemon=True)
@@ -36,11 +38,19 @@ class MicroBatcher:
     def submit(self, pixel_values: torch.Tensor) -> Future:
         """Queue a [n,3,H,W] batch; the Future resolves to its (logits, boxes) rows (owned copies)."""
         fut: Future = Future()
+        with self._pending_lock:
+            self._pending += 1
         self._q.put((pixel_values, fut))
         return fut
 
     def __call__(self, pixel_values: torch.Tensor):
         return self.submit(pixel_values).result()
+
+    def _others_waiting(self, taken: int) -> bool:
+        """True while some submitted image is not among the `taken` ones: only then is waiting for
+        more worth anything. (The collector resolves every future itself, so the count is exact.)"""
+        with self._pending_lock:
+            return self._pending > taken
 
     def _take(self):
         first = self._q.get()
@@ -52,6 +62,8 @@ class MicroBatcher:
         deadline = time.perf_counter() + self.max_wait
         held = []
         while n < self.max_batch:
+            if not self._others_waiting(len(items)):
+                break  # a lone serial caller (the unchanged serve.py) is dispatched at once
             left = deadline - time.perf_counter()
             if left <= 0:
                 break
@@ -92,9 +104,13 @@ class MicroBatcher:
                     off += k
                 if self.device.type == "cuda":
                     torch.cuda.current_stream().synchronize()
+                with self._pending_lock:
+                    self._pending -= len(items)
                 for fut, lg, bx in outs:
                     fut.set_result((lg, bx))
             except BaseException as e:  # every waiting caller sees the failure
+                with self._pending_lock:
+                    self._pending -= sum(1 for _, f in items if not f.done())
                 for _, fut in items:
                     if not fut.done():
                         fut.set_exception(e)

@@ -1,8 +1,14 @@
-"""Real-weight loader from a LOCAL directory: config.json +
-model.safetensors in HF layout. 4.x key names are mapped to the 5.x names the
-engine uses (transformers/conversion_mapping.py:1042-1047: out_proj→o_proj,
+"""Real-weight loader: config.json + model.safetensors in HF layout,
+from a local directory or from the local HF hub cache. 4.x key names are mapped to the
+5.x names the engine uses (transformers/conversion_mapping.py:1042-1047: out_proj→o_proj,
 layers.N.fc1/fc2→layers.N.mlp.fc1/fc2, encoder.encoder.N.layers→encoder.aifi.N.layers).
-Nothing is fetched; a hub name never reaches this module.
+
+Hub names resolve the way `from_pretrained` resolves them offline: the reference image
+pre-downloads MODEL_NAME into the HF cache at build time (reference
+apps/spotter/Dockerfile:17 → src/spotter/download.py:23-27) and serve.py:203-204 loads
+it by the same name. `resolve_pretrained` finds that snapshot
+(<cache>/models--{org}--{name}/snapshots/<refs/main>/); nothing is fetched, and a name
+that is not in the cache raises instead of running other weights.
 """
 from __future__ import annotations
 
@@ -62,6 +68,21 @@ _IGNORED = {
     "_name_or_path", "backbone_config", "backbone", "use_timm_backbone", "use_pretrained_backbone",
     "backbone_kwargs", "return_dict", "output_hidden_states", "output_attentions", "use_return_dict",
     "pruned_heads", "chunk_size_feed_forward", "problem_type", "tokenizer_class", "num_labels",
+}
+
+
+# Generic PretrainedConfig attributes (generation / bookkeeping; configuration_utils.py) that some
+# transformers versions write on save_pretrained. Underscore-prefixed bookkeeping keys
+# (_attn_implementation_autoset, _commit_hash, …) are skipped by prefix.
+_GENERIC = {
+    "add_cross_attention", "bad_words_ids", "begin_suppress_tokens", "bos_token_id", "cross_attention_hidden_size",
+    "decoder_start_token_id", "diversity_penalty", "do_sample", "early_stopping", "encoder_no_repeat_ngram_size",
+    "eos_token_id", "exponential_decay_length_penalty", "finetuning_task", "forced_bos_token_id",
+    "forced_eos_token_id", "is_decoder", "length_penalty", "max_length", "min_length", "no_repeat_ngram_size",
+    "num_beam_groups", "num_beams", "num_return_sequences", "output_scores", "pad_token_id", "prefix",
+    "remove_invalid_values", "repetition_penalty", "return_dict_in_generate", "sep_token_id", "suppress_tokens",
+    "task_specific_params", "temperature", "tf_legacy_loss", "tie_encoder_decoder", "top_k", "top_p",
+    "torchscript", "typical_p", "use_bfloat16", "label_smoothing", "use_cache",
 }
 
 
@@ -156,7 +177,56 @@ def unknown_fields(js: dict) -> list:
             "decoder_activation_function", "decoder_layers", "decoder_attention_heads", "decoder_n_levels",
             "num_feature_levels", "decoder_n_points", "decoder_offset_scale", "num_queries", "anchor_image_size",
             "layer_norm_eps", "batch_norm_eps", "hidden_size", "num_attention_heads"}
-    return sorted(k for k in js if k not in read and k not in _FIXED and k not in _IGNORED)
+    return sorted(k for k in js if k not in read and k not in _FIXED and k not in _IGNORED
+                  and k not in _GENERIC and not k.startswith("_"))
+
+
+def hub_cache_dirs() -> list:
+    """The HF hub cache directories `from_pretrained` would look in, in huggingface_hub's order
+    (constants.py: HF_HUB_CACHE, else HF_HOME/hub, else ~/.cache/huggingface/hub; the
+    deprecated TRANSFORMERS_CACHE / HUGGINGFACE_HUB_CACHE names too)."""
+    out = []
+    for var in ("HF_HUB_CACHE", "HUGGINGFACE_HUB_CACHE", "TRANSFORMERS_CACHE"):
+        if os.environ.get(var):
+            out.append(os.path.expanduser(os.environ[var]))
+    home = os.environ.get("HF_HOME") or os.path.join(
+        os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache"), "huggingface")
+    out.append(os.path.join(os.path.expanduser(home), "hub"))
+    seen = []
+    for d in out:
+        if d not in seen:
+            seen.append(d)
+    return seen
+
+
+def resolve_pretrained(name_or_path: str, revision: str = "main", need: str = "config.json") -> str:
+    """A local directory → itself; a hub repo id ("PekingU/rtdetr_v2_r101vd") → its snapshot
+    directory in the local HF cache (refs/<revision> → snapshots/<commit>, or a commit hash given
+    as revision). Raises OSError naming the searched paths when no snapshot holding `need` exists:
+    there is no network and no silent substitute."""
+    if os.path.isdir(name_or_path):
+        return name_or_path
+    repo = name_or_path.strip("/")
+    if repo.count("/") > 1 or not repo:
+        raise OSError(f"{name_or_path!r} is neither a local directory nor a hub repo id")
+    folder = "models--" + repo.replace("/", "--")
+    tried = []
+    for cache in hub_cache_dirs():
+        base = os.path.join(cache, folder)
+        tried.append(base)
+        if not os.path.isdir(base):
+            continue
+        commit = revision
+        ref = os.path.join(base, "refs", revision)
+        if os.path.isfile(ref):
+            with open(ref) as f:
+                commit = f.read().strip()
+        snap = os.path.join(base, "snapshots", commit)
+        if os.path.isfile(os.path.join(snap, need)):
+            return snap
+    raise OSError(f"{name_or_path!r}: no local directory and no cached snapshot with {need} "
+                  f"(searched {tried}; nothing is downloaded — pre-fetch it as the reference's "
+                  f"download.py does, or pass a checkpoint directory)")
 
 
 def load_local(path: str):
@@ -166,7 +236,12 @@ def load_local(path: str):
         js = json.load(f)
     unk = unknown_fields(js)
     if unk:
-        raise UnsupportedConfig(f"config.json fields this loader does not know: {unk}")
+        # not an inference field this loader knows: the _FIXED and activation fields are refused
+        # hard by config_from_hf; anything else is reported, not fatal
+        import warnings
+
+        warnings.warn(f"config.json fields this loader does not read (assumed not to change inference): {unk}",
+                      stacklevel=2)
     cfg = config_from_hf(js)
     raw = {}
     for fn in sorted(os.listdir(path)):

@@ -72,21 +72,23 @@ def _wkw(wq):
 
 
 class ConvW:
-    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16", "host", "wino")
+    __slots__ = ("w", "cin", "cout", "k", "scale", "shift", "w16", "host", "wino", "mode")
 
-    def __init__(self, w, cin, cout, k, scale, shift, w16=None, host=None):
+    def __init__(self, w, cin, cout, k, scale, shift, w16=None, host=None, mode="f32"):
         self.w, self.cin, self.cout, self.k, self.scale, self.shift = w, cin, cout, k, scale, shift
         self.w16 = w16
+        self.mode = mode  # operand mode of w16: "f32" (none: fp32 MFMA), "bf16" (one plane), "x3" (three)
         self.host = host  # the packed fp32 [Cout, K] weights on the host (pack-time fusions read them)
         self.wino = None  # Winograd F(2x2, 3x3) weight planes when this stride-1 3x3 runs that way
 
 
 class LinW:
-    __slots__ = ("w", "b", "k", "n", "w16")
+    __slots__ = ("w", "b", "k", "n", "w16", "mode")
 
-    def __init__(self, w, b, k, n, w16=None):
+    def __init__(self, w, b, k, n, w16=None, mode="f32"):
         self.w, self.b, self.k, self.n = w, b, k, n
         self.w16 = w16
+        self.mode = mode  # as ConvW.mode
 
 
 def frozen_bn_affine(p, pre):
@@ -215,13 +217,12 @@ class Engine:
         """Attach the F(2x2, 3x3) transformed weight planes (host fp64 transform, then the conv's own
         operand form: three split planes or one bf16 plane) to a stride-1 3x3 conv the Winograd policy
         (self.winograd) selects."""
-        if cw.k != 3 or cw.w16 is None or cw.cin % 32 or cw.cout % 4 or not self.winograd:
+        if cw.k != 3 or cw.mode == "f32" or cw.cin % 32 or cw.cout % 4 or not self.winograd:
             return cw
-        planes = cw.w16.shape[0] if cw.w16.dim() == 2 else 1
-        if self.winograd == "auto" and (cw.cin < (128 if self.wino_m == 4 else 256) or planes != 3):
+        if self.winograd == "auto" and (cw.cin < (128 if self.wino_m == 4 else 256) or cw.mode != "x3"):
             return cw
         u = ops.winograd_weights_host(cw.host.reshape(cw.cout, 3, 3, cw.cin), self.wino_m)
-        if planes == 3:
+        if cw.mode == "x3":
             cw.wino = torch.from_numpy(ops.split_bf16x3_host(u)).to(self.dev)
         else:
             cw.wino = torch.from_numpy(bf16_bits(u).reshape(1, -1).view(np.int16)).to(self.dev)
@@ -242,8 +243,9 @@ class Engine:
 
     def _mk_conv(self, wk, ci, co, k, sc, sh):
         wk = np.ascontiguousarray(wk, dtype=np.float32)
-        return ConvW(_t(wk, self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev),
-                     self._wq(wk, self._pick(self._conv_mode, co, ci * k * k)), host=wk)
+        mode = self._pick(self._conv_mode, co, ci * k * k)
+        return ConvW(_t(wk, self.dev), ci, co, k, _t(sc, self.dev), _t(sh, self.dev), self._wq(wk, mode), host=wk,
+                     mode=mode)
 
     def _conv(self, p, conv_key, bn_pre, frozen):
         w = p[conv_key]
@@ -260,7 +262,7 @@ class Engine:
         b = np.concatenate(bs, 0)
         wd = _t(w, self.dev)
         mode = self._pick(self._lin_mode, w.shape[0], w.shape[1], small_m=per_query and w.shape[0] > 128)
-        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(w.astype(np.float32), mode))
+        return LinW(wd, _t(b, self.dev), w.shape[1], w.shape[0], self._wq(w.astype(np.float32), mode), mode=mode)
 
     def _ln(self, p, pre):
         return (_t(p[pre + ".weight"], self.dev), _t(p[pre + ".bias"], self.dev))
@@ -365,7 +367,7 @@ class Engine:
         w12 = np.concatenate([conv_khwc(w1), conv_khwc(w2)], 0)
         c12 = ConvW(_t(w12, self.dev), w1.shape[1], w1.shape[0] + w2.shape[0], 1,
                     _t(np.concatenate([s1, s2]), self.dev), _t(np.concatenate([b1, b2]), self.dev),
-                    self._wq(w12, self._conv_mode), host=w12)
+                    self._wq(w12, self._conv_mode), host=w12, mode=self._conv_mode)
         reps = []
         for b in range(3):
             q = f"{pre}.bottlenecks.{b}"
@@ -438,6 +440,13 @@ class Engine:
         """ln = (gamma, beta): the post-norm LayerNorm of the output row fused into the GEMM epilogue
         (fp32-MFMA tile holding whole rows; sp_conv_desc.ln_gamma)."""
         if ln is not None and self.fuse_ln:
+            # the fused-LN tile runs on the fp32 weights (fp32 MFMA): exact for the fp32-accurate modes,
+            # but it would silently raise a bf16 layer's operand precision, and its epilogue has no act /
+            # post-act residual: refuse rather than drop either
+            if act is not None or res2 is not None:
+                raise ValueError("fused LayerNorm epilogue: act / res2 are not implemented")
+            if lw.mode == "bf16":
+                raise ValueError("fuse_ln runs fp32 weights: not available on a bf16-operand layer")
             return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, res1=res1, a2=a2, row_scale=row_scale,
                               ln=(ln[0], ln[1], self.cfg.layer_norm_eps))
         if ln is not None:  # unfused: GEMM into a scratch row block, then sp_layernorm into `out`

@@ -10,7 +10,6 @@ first call, from the host-side weight dictionary.
 """
 from __future__ import annotations
 
-import os
 import threading
 from dataclasses import dataclass
 
@@ -73,19 +72,22 @@ class SpotterForObjectDetection:
 
     # -- construction -------------------------------------------------------------
     @classmethod
-    def from_pretrained(cls, name_or_path: str = "PekingU/rtdetr_v2_r101vd", **kw):
-        """Local directory with HF weights → those weights (spotter_amd.checkpoint);
-        anything else (a hub name; no network here) → the preset's deterministic synthetic weights."""
-        if os.path.isdir(name_or_path):
-            from .checkpoint import load_local
+    def from_pretrained(cls, name_or_path: str = "PekingU/rtdetr_v2_r101vd", synthetic: bool = False,
+                        revision: str = "main", **kw):
+        """What HF `from_pretrained` loads, offline: a local checkpoint directory, or a hub repo id
+        resolved to its snapshot in the local HF cache (the reference image pre-fetches MODEL_NAME
+        there: apps/spotter/Dockerfile:17 → download.py:23-27). A name that resolves to nothing
+        raises OSError, as HF does offline. Deterministic synthetic weights only on explicit opt-in:
+        `synthetic=True`, or a name of the form "synthetic:<preset>" (e.g. via MODEL_NAME)."""
+        if name_or_path.startswith("synthetic:"):
+            synthetic, name_or_path = True, name_or_path[len("synthetic:"):]
+        if synthetic:
+            preset = name_or_path if name_or_path in PRESETS else _preset_for(name_or_path).name
+            return cls(PRESETS[preset], None, **kw)
+        from .checkpoint import load_local, resolve_pretrained
 
-            cfg, weights = load_local(name_or_path)
-            return cls(cfg, weights, **{k: v for k, v in kw.items() if k != "seed"})
-        import warnings
-
-        warnings.warn(f"{name_or_path!r} is not a local checkpoint directory (nothing is fetched): using the "
-                      f"{_preset_for(name_or_path).name} preset with deterministic SYNTHETIC weights", stacklevel=2)
-        return cls(_preset_for(name_or_path), None, **kw)
+        cfg, weights = load_local(resolve_pretrained(name_or_path, revision=revision))
+        return cls(cfg, weights, **{k: v for k, v in kw.items() if k != "seed"})
 
     def _host_weights(self):
         if self._weights is None:
@@ -142,9 +144,16 @@ class SpotterForObjectDetection:
                     if self._batcher is None:
                         from .batching import MicroBatcher
 
-                        self._batcher = MicroBatcher(eng.forward, eng.dev, self.max_batch, self.max_wait_ms)
-            logits, boxes = self._batcher(pixel_values.float())
+                        self._batcher = MicroBatcher(self._run, eng.dev, self.max_batch, self.max_wait_ms)
+            logits, boxes = self._batcher(pixel_values.float())  # the batcher hands out owned rows
             return SpotterDetectionOutput(logits=logits, pred_boxes=boxes)
+        logits, boxes = self._run(pixel_values)
+        # own copies: the engine reuses its workspace on the next call
+        return SpotterDetectionOutput(logits=logits.clone(), pred_boxes=boxes.clone())
+
+    def _run(self, pixel_values):
+        """One forward on the engine's stream; outputs live in engine / graph buffers until the next call."""
+        eng = self.engine
         key = tuple(pixel_values.shape)
         if self.use_graphs and key[0] <= 4:
             # small batches are launch-bound: replay a captured hipGraph of the whole forward
@@ -156,10 +165,7 @@ class SpotterForObjectDetection:
                 g = self._graphs[key] = GraphRunner(eng, *key[:1], *key[2:])
             self._seen.add(key)
             if g is not None:
-                logits, boxes = g(pixel_values.float())
-                return SpotterDetectionOutput(logits=logits.clone(), pred_boxes=boxes.clone())
-        logits, boxes = eng.forward(pixel_values)
-        # own copies: the engine reuses its workspace on the next call
-        return SpotterDetectionOutput(logits=logits.clone(), pred_boxes=boxes.clone())
+                return g(pixel_values.float())
+        return eng.forward(pixel_values)
 
     forward = __call__

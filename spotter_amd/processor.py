@@ -72,20 +72,66 @@ class SpotterImageProcessor:
             raise NotImplementedError("only the RT-DETR defaults (resize, rescale 1/255, no normalize/pad) are on the HIP path")
         if abs(self.rescale_factor - 1 / 255) > 1e-12:
             raise NotImplementedError("rescale_factor must be 1/255")
+        # PIL.Image.BILINEAR == 2 (IPP:129-143 default); the kernel is Pillow's bilinear resample only
+        self.resample = kwargs.get("resample", 2)
+        if self.resample not in (2, "bilinear", "BILINEAR"):
+            raise NotImplementedError(f"resample={self.resample!r}: the HIP preprocess implements PIL BILINEAR (2) only")
+        if not {"height", "width"} <= set(self.size):
+            raise NotImplementedError(f"size={self.size!r}: only an explicit {{height, width}} resize is on the HIP path")
         self.device = device
+        self._stage = None  # pinned host staging buffer, reused across calls
+        self._stage_done = None  # event after the last H2D copy out of it
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_stage"] = None
+        st["_stage_done"] = None
+        return st
 
     @classmethod
     def from_pretrained(cls, path_or_name, **kwargs):
+        """A local directory or a hub repo id cached locally (checkpoint.resolve_pretrained: the
+        reference's download.py:29-30 pre-fetches the processor config under the same name);
+        preprocessor_config.json fields that change the arithmetic are honoured or refused.
+        "synthetic:<preset>" → the RT-DETR defaults (explicit opt-in, as for the model)."""
         cfg = {}
-        if os.path.isdir(path_or_name):
-            p = os.path.join(path_or_name, "preprocessor_config.json")
+        if not str(path_or_name).startswith("synthetic:"):
+            from .checkpoint import resolve_pretrained
+
+            d = resolve_pretrained(path_or_name, need="preprocessor_config.json") if not os.path.isdir(
+                path_or_name) else path_or_name
+            p = os.path.join(d, "preprocessor_config.json")
             if os.path.exists(p):
                 with open(p) as f:
                     cfg = json.load(f)
         cfg.update(kwargs)
         keep = {k: cfg[k] for k in ("size", "do_resize", "do_rescale", "do_normalize", "do_pad",
-                                     "rescale_factor") if k in cfg}
+                                     "rescale_factor", "resample") if k in cfg}
         return cls(**keep)
+
+    def _upload(self, arrs, dev):
+        """Decoded uint8 images → device, through one reused pinned staging buffer (no per-request
+        pinned allocation): wait for the previous copy out of it, fill it, one async H2D per image."""
+        sizes = [a.size for a in arrs]
+        offs, total = [], 0
+        for n in sizes:  # 256-B aligned slots (the same-size kernel reads 4-byte words)
+            offs.append(total)
+            total += (n + 255) & ~255
+        if self._stage_done is not None:
+            self._stage_done.synchronize()
+        if self._stage is None or self._stage.numel() < total:
+            self._stage = torch.empty((max(total, 1 << 20),), dtype=torch.uint8, pin_memory=True)
+        dst = torch.empty((total,), dtype=torch.uint8, device=dev)
+        host = self._stage.numpy()
+        ups = []
+        for a, n, off in zip(arrs, sizes, offs):
+            host[off:off + n] = a.reshape(-1)
+            ups.append(dst[off:off + n].view(a.shape))
+        dst.copy_(self._stage[:total], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        self._stage_done = ev
+        return ups
 
     def _dev(self):
         if self.device is not None:
@@ -101,7 +147,7 @@ class SpotterImageProcessor:
         dev = self._dev()
         oh, ow = int(self.size["height"]), int(self.size["width"])
         with torch.cuda.device(dev):
-            ups = [torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(dev, non_blocking=True) for a in arrs]
+            ups = self._upload(arrs, dev)
             out = torch.empty((len(arrs), 3, oh, ow), dtype=torch.float32, device=dev)
             ops.preprocess_u8(ups, out, oh, ow)
         if return_tensors not in ("pt", None):

@@ -65,14 +65,23 @@ def _stub_modules():
     return {"ray": ray, "ray.serve": serve, "tenacity": ten}
 
 
-def _load_patched_serve(monkeypatch):
-    src = open(os.path.join(REF, "serve.py")).read()
-    old_model = "model = AutoModelForObjectDetection.from_pretrained(model_name).to(device)  # type: ignore"
-    old_proc = "processor = AutoImageProcessor.from_pretrained(model_name)"
-    assert old_model in src and old_proc in src, "reference serve.py changed; update INTEGRATION.md"
-    src = src.replace(old_model, "from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor\n"
-                                 "model = SpotterForObjectDetection.from_pretrained(model_name).to(device)")
-    src = src.replace(old_proc, "processor = SpotterImageProcessor.from_pretrained(model_name)")
+def _load_patched_serve(monkeypatch, tmp_path):
+    """The reference serve.py with the drop-in applied by the same code the image runs
+    (spotter_amd.dropin, deploy/Dockerfile.rocm), MODEL_NAME = the reference's hub name, resolved
+    from a local HF cache snapshot (an R18 checkpoint stored under that name keeps the test small)."""
+    from spotter_amd.checkpoint import save_local
+    from spotter_amd.config import PRESETS
+    from spotter_amd.dropin import patch_source
+    from spotter_amd.weights import generate
+
+    src = patch_source(open(os.path.join(REF, "serve.py")).read())
+    base = tmp_path / "hub" / "models--PekingU--rtdetr_v2_r101vd"
+    save_local(str(base / "snapshots" / "c0ffee"), PRESETS["r18vd"], generate(PRESETS["r18vd"], seed=0))
+    (base / "snapshots" / "c0ffee" / "preprocessor_config.json").write_text(
+        '{"do_resize": true, "size": {"height": 640, "width": 640}, "resample": 2, "do_rescale": true}')
+    (base / "refs").mkdir(parents=True)
+    (base / "refs" / "main").write_text("c0ffee")
+    monkeypatch.setenv("HF_HUB_CACHE", str(tmp_path / "hub"))
     for name, mod in _stub_modules().items():
         monkeypatch.setitem(sys.modules, name, mod)
     pkg = types.ModuleType("spotter")
@@ -90,28 +99,29 @@ def _load_patched_serve(monkeypatch):
     return mod, schemas
 
 
-def test_reference_deployment_module_binds_our_objects(monkeypatch):
+def test_reference_deployment_module_binds_our_objects(monkeypatch, tmp_path):
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
 
-    serve, _ = _load_patched_serve(monkeypatch)
+    serve, _ = _load_patched_serve(monkeypatch, tmp_path)
     assert isinstance(serve.model, SpotterForObjectDetection)
     assert isinstance(serve.processor, SpotterImageProcessor)
     kind, cls, blob = serve.deployment
     assert kind == "bound" and cls.__name__ == "AmenitiesDetector"
     (m, p), _ = pickle.loads(blob)  # what Ray ships to each replica: no device state inside
     assert m._engine is None and m.config.id2label[62] == "tv"
+    assert m.cfg.depths == [2, 2, 2, 2] and m._weights is not None  # the cached snapshot, not a preset
     det = cls(model=m, processor=p)  # serve.py:66-72 constructor check passes
     assert det.processor is p
 
 
-def test_reference_process_single_image_flow_with_our_types(monkeypatch):
+def test_reference_process_single_image_flow_with_our_types(monkeypatch, tmp_path):
     """serve.py:79-148 with our model/processor; kernels replaced by canned outputs (CPU only)."""
     import torch
 
     from spotter_amd import SpotterImageProcessor
     from spotter_amd.model import SpotterDetectionOutput
 
-    serve, schemas = _load_patched_serve(monkeypatch)
+    serve, schemas = _load_patched_serve(monkeypatch, tmp_path)
     cls = serve.deployment[1]
     det = cls(model=serve.model, processor=serve.processor)
     det.client = AsyncMock()

@@ -91,8 +91,8 @@ def test_dropin_interface_and_pickling():
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
     from spotter_amd.processor import SpotterBatchFeature
 
-    proc = SpotterImageProcessor.from_pretrained("PekingU/rtdetr_v2_r101vd")
-    model = SpotterForObjectDetection.from_pretrained("PekingU/rtdetr_v2_r101vd").to(torch.device("cpu"))
+    proc = SpotterImageProcessor.from_pretrained("synthetic:r101vd")
+    model = SpotterForObjectDetection.from_pretrained("synthetic:r101vd").to(torch.device("cpu"))
     assert hasattr(proc, "post_process_object_detection")
     assert model.config.id2label[62] == "tv" and model.config.id2label[57] == "couch"
     assert model.config.id2label[60] == "dining table" and model.config.id2label[78] == "hair drier"
@@ -236,6 +236,96 @@ def test_local_checkpoint_round_trip(tmp_path):
     assert all(np.array_equal(w2[k], w[k]) for k in w)
 
 
+def _fake_hub_cache(root, repo, cfg, weights, commit="0123abcd"):
+    """A HF hub cache entry laid out as huggingface_hub writes it: refs/main → snapshots/<commit>/."""
+    import json
+
+    from spotter_amd.checkpoint import save_local
+
+    base = root / ("models--" + repo.replace("/", "--"))
+    snap = base / "snapshots" / commit
+    save_local(str(snap), cfg, weights)
+    (snap / "preprocessor_config.json").write_text(json.dumps(
+        {"image_processor_type": "RTDetrImageProcessor", "do_resize": True, "size": {"height": 640, "width": 640},
+         "resample": 2, "do_rescale": True, "rescale_factor": 1 / 255, "do_normalize": False, "do_pad": False,
+         "format": "coco_detection", "do_convert_annotations": True}))
+    (base / "refs").mkdir(parents=True)
+    (base / "refs" / "main").write_text(commit)
+    return snap
+
+
+def test_hub_name_resolves_to_the_cached_snapshot(tmp_path, monkeypatch):
+    """from_pretrained(<hub name>) loads the snapshot HF's cache holds under that name (the reference
+    image pre-fetches MODEL_NAME there: apps/spotter/Dockerfile:17 → download.py:23-27, then
+    serve.py:203-204 loads it by name): same config and tensors, and the processor reads the
+    snapshot's preprocessor_config.json. A name not in the cache raises; synthetic is opt-in only."""
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.checkpoint import resolve_pretrained
+    from spotter_amd.config import PRESETS
+    from spotter_amd.weights import generate
+
+    cfg = PRESETS["r18vd"]
+    w = generate(cfg, seed=5)
+    snap = _fake_hub_cache(tmp_path / "hub", "PekingU/rtdetr_v2_r101vd", cfg, w)
+    for var in ("HF_HUB_CACHE", "HUGGINGFACE_HUB_CACHE", "TRANSFORMERS_CACHE"):
+        monkeypatch.delenv(var, raising=False)
+    monkeypatch.setenv("HF_HOME", str(tmp_path))
+    assert resolve_pretrained("PekingU/rtdetr_v2_r101vd") == str(snap)
+    m = SpotterForObjectDetection.from_pretrained("PekingU/rtdetr_v2_r101vd")
+    assert m.cfg.depths == cfg.depths and set(m._weights) == set(w)
+    assert all(np.array_equal(m._weights[k], w[k]) for k in w)
+    p = SpotterImageProcessor.from_pretrained("PekingU/rtdetr_v2_r101vd")
+    assert p.size == {"height": 640, "width": 640} and p.resample == 2
+    with pytest.raises(OSError, match="no local directory and no cached snapshot"):
+        SpotterForObjectDetection.from_pretrained("PekingU/rtdetr_v2_r50vd")
+    with pytest.raises(OSError):
+        SpotterImageProcessor.from_pretrained("PekingU/rtdetr_v2_r50vd")
+    monkeypatch.setenv("HF_HUB_CACHE", str(tmp_path / "hub"))  # the explicit cache variable
+    monkeypatch.setenv("HF_HOME", str(tmp_path / "elsewhere"))
+    assert resolve_pretrained("PekingU/rtdetr_v2_r101vd") == str(snap)
+    assert SpotterForObjectDetection.from_pretrained("synthetic:r101vd")._weights is None
+    assert SpotterForObjectDetection.from_pretrained("x", synthetic=True).cfg.name == "r101vd"
+
+
+def test_processor_refuses_arithmetic_it_does_not_implement(tmp_path):
+    """preprocessor_config.json fields that change the arithmetic are honoured or refused, never ignored."""
+    import json
+
+    from spotter_amd import SpotterImageProcessor
+
+    for bad in ({"resample": 3}, {"resample": 0}, {"do_normalize": True}, {"do_pad": True},
+                {"rescale_factor": 1 / 127.5}, {"size": {"shortest_edge": 640}}):
+        d = tmp_path / ("c%d" % len(list(tmp_path.iterdir())))
+        d.mkdir()
+        (d / "preprocessor_config.json").write_text(json.dumps(dict({"resample": 2}, **bad)))
+        with pytest.raises(NotImplementedError):
+            SpotterImageProcessor.from_pretrained(str(d))
+    ok = tmp_path / "ok"
+    ok.mkdir()
+    (ok / "preprocessor_config.json").write_text(json.dumps({"resample": 2, "size": {"height": 800, "width": 800}}))
+    assert SpotterImageProcessor.from_pretrained(str(ok)).size == {"height": 800, "width": 800}
+
+
+def test_loader_skips_bookkeeping_keys_and_warns_on_unknown(tmp_path):
+    """Keys some transformers versions add on save (underscore bookkeeping, generic PretrainedConfig
+    attributes) do not stop a real checkpoint from loading; an unknown key is reported, not fatal."""
+    import json
+
+    from spotter_amd.checkpoint import hf_config_dict, load_local, unknown_fields
+    from spotter_amd.config import PRESETS
+
+    js = hf_config_dict(PRESETS["r18vd"])
+    js.update(_attn_implementation_autoset=True, _commit_hash="abc", use_cache=True, pad_token_id=None,
+              output_scores=False)
+    assert unknown_fields(js) == []
+    js["some_future_field"] = 1
+    assert unknown_fields(js) == ["some_future_field"]
+    (tmp_path / "config.json").write_text(json.dumps(js))
+    with pytest.warns(UserWarning, match="some_future_field"):
+        cfg, w = load_local(str(tmp_path))
+    assert cfg.depths == PRESETS["r18vd"].depths and w == {}
+
+
 @pytest.mark.parametrize("wm", [2, 4])
 def test_winograd_weight_transform_reproduces_the_direct_conv(wm):
     """ops.winograd_weights_host (U = G g Gᵀ, fp64 on the host) composed with the F(m×m,3x3) input /
@@ -355,6 +445,39 @@ def test_dockerfile_copies_exist_in_their_contexts():
                 assert os.path.exists(os.path.join(ref, s)), s
     stages = [l.split()[-1] for l in lines if l.startswith("FROM ")]
     assert {"checkpoint", "spotter_amd"} <= set(stages)
+    text = "\n".join(lines)
+    # the image applies and verifies the drop-in itself (no hand edit of serve.py before docker build)
+    assert "python -m spotter_amd.dropin src/spotter/serve.py" in text and "d.check(" in text
+    assert text.index("spotter_amd.dropin src/spotter/serve.py") > text.index("COPY apps/spotter/src ./src")
+
+
+def test_dropin_script_patches_serve_py(tmp_path):
+    """spotter_amd.dropin (run by the Dockerfile) on a copy of the reference serve.py: the two lines of
+    serve.py:203-204 are replaced, a second run is a no-op, and a serve.py whose lines moved is refused."""
+    import sys
+
+    from spotter_amd import dropin
+
+    ref = "/root/reference/apps/spotter/src/spotter/serve.py"
+    if os.path.exists(ref):
+        src = open(ref).read()
+    else:  # the GPU box has no reference: the two lines as the reference writes them
+        src = f"import os\nmodel_name = os.environ.get('MODEL_NAME')\n{dropin.OLD_MODEL}\n{dropin.OLD_PROC}\n"
+    p = tmp_path / "serve.py"
+    p.write_text(src)
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-m", "spotter_amd.dropin", str(p)], cwd=ROOT, capture_output=True,
+                           text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+    out = p.read_text()
+    dropin.check(out)
+    assert out.count("SpotterForObjectDetection.from_pretrained(model_name)") == 1
+    assert out.replace(dropin.NEW_MODEL, dropin.OLD_MODEL).replace(dropin.NEW_PROC, dropin.OLD_PROC) == src
+    bad = tmp_path / "bad.py"
+    bad.write_text(src.replace(dropin.OLD_PROC, "processor = AutoImageProcessor.from_pretrained(other)"))
+    r = subprocess.run([sys.executable, "-m", "spotter_amd.dropin", str(bad)], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "expected exactly one" in r.stderr
 
 
 def test_detect_path_harness_with_fake_model():
@@ -455,3 +578,39 @@ def test_microbatcher_coalesces_concurrent_calls():
         mb2(torch.zeros(1, 3, 8, 8))
     mb.close()
     mb2.close()
+
+
+def test_microbatcher_lone_serial_caller_is_not_delayed():
+    """The unchanged serve.py calls the model once per image, serially: with nobody else pending the
+    batcher dispatches at once instead of waiting max_wait_ms for company."""
+    import time
+
+    import torch
+
+    from spotter_amd.batching import MicroBatcher
+
+    mb = MicroBatcher(lambda x: (x[:, :1, 0, :3], x[:, 0, :1, :4]), "cpu", max_batch=32, max_wait_ms=200)
+    x = torch.zeros(1, 3, 8, 8)
+    mb(x)  # thread warm-up
+    t0 = time.perf_counter()
+    for _ in range(20):
+        mb(x)
+    per_call = (time.perf_counter() - t0) / 20
+    mb.close()
+    assert per_call < 0.05, per_call  # far below the 200 ms wait window
+    assert mb.batches == 21 and mb._pending == 0
+
+
+def test_tile_table_entries_can_run_their_configuration():
+    """Every exact-shape entry of csrc/tile_table.h names a configuration its shape can launch (the LDS-DMA
+    tiles need Cin % BK == 0): an entry the generic kernel would shadow is dead weight."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from gen_tile_table import runnable
+
+    src = open(os.path.join(ROOT, "spotter_amd", "csrc", "tile_table.h")).read()
+    rows = [tuple(map(int, m)) for m in re.findall(r"\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (-?\d+)\},", src)]
+    assert len(rows) > 50
+    bad = [r for r in rows if r[0] and r[5] and not runnable(r[6], r[2] // (r[3] * r[3]), r[1])]
+    assert bad == []
