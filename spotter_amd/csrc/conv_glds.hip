@@ -33,7 +33,12 @@ struct GldsCfg {
 
 // The LDS-DMA main loop of one output tile: k-tiles [kt0, kt1) of tile `wg` (N fastest) accumulated
 // into acc (acc4 for 16x16x32 MFMAs). The caller zeroes the accumulators and owns the epilogue.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
+// V (variant): 0 = element-wise split, per-piece 64-bit addresses with tap walk and bounds selects;
+// 1 = pair-wise split (split_frag_pk: the minimum VALU stream); 2 = 1 + the 1×1 fast path (KH = KW = 1,
+// stride 1, no padding, A / weight byte offsets < 4 GiB): per-lane 32-bit offsets against SGPR bases
+// that advance by one scalar add per k-step (glds16s); rows past M / columns past Cout re-read the last
+// valid row / column (their outputs are masked in the epilogue) instead of a zero block.
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 0>
 __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
                                           f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
@@ -86,6 +91,20 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     b_ptr[j] = Wt + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
   }
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+  // V == 2: byte offsets of this lane's A rows / B rows against the operand bases
+  uint32_t a_off[V == 2 ? GA : 1], b_off[V == 2 ? GB : 1];
+  if constexpr (V == 2) {
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int64_t m = m0 + (j * NT + tid) / RA;
+      a_off[j] = (uint32_t)(((m < p.M ? m : p.M - 1) * d.lda + ca * 4) * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int n = n0 + (j * NT + tid) / RB;
+      b_off[j] = (uint32_t)(((int64_t)(n < d.Cout ? n : d.Cout - 1) * p.K + cbk * 8) * 2);
+    }
+  }
 
   int s_kh = 0, s_kw = 0, s_c0 = 0;
   const int nk = kt1 - kt0;
@@ -102,6 +121,18 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
   auto issue = [&](int kt, int buf) {
     const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
+    if constexpr (V == 2) {
+      const float* ab = A + (int64_t)kt * BK;
+#pragma unroll
+      for (int j = 0; j < GA; ++j) glds16s(a_off[j], ab, st + j * NT * 16);
+#pragma unroll
+      for (int pl = 0; pl < PL; ++pl) {
+        const uint16_t* bb = Wt + pl * wps + (int64_t)kt * BK;
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16s(b_off[j], bb, st + (CA + pl * CB + j * NT) * 16);
+      }
+      return;
+    }
     const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
 #pragma unroll
     for (int j = 0; j < GA; ++j) {
@@ -154,7 +185,8 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
         bf16x8 fa[PL];
-        split_frag<PL>(x0, x1, fa);
+        if constexpr (V >= 1) split_frag_pk<PL>(x0, x1, fa);
+        else split_frag<PL>(x0, x1, fa);
 #pragma unroll
         for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
       }
@@ -187,7 +219,8 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
           for (int q = 0; q < PL; ++q) fa[q] = hh;
         }
 #else
-        split_frag<PL>(x0, x1, fa);
+        if constexpr (V >= 1) split_frag_pk<PL>(x0, x1, fa);
+        else split_frag<PL>(x0, x1, fa);
 #endif
 #if SP_ABLATE == 3  // no MFMA: keep the operands alive
 #pragma unroll
@@ -269,7 +302,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
                                     n0 + wn * TN * 32, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 0>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
   __shared__ uint4 smem[C::SMEM];
@@ -283,14 +316,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
   f32x16 acc[TM][TN];
   f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   glds_zero<TM, TN, M16>(acc, acc4);
-  glds_main<WM, WN, TM, TN, PL, NS, BK, M16>(p, smem, wg, bi, kt0, kt1, acc, acc4);
+  glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V>(p, smem, wg, bi, kt0, kt1, acc, acc4);
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   ConvArgs q = p;
   q.d.C += (int64_t)bi * p.bs_c;
   glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(q, smem, wg, acc, acc4);
 }
 
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
+// The 1×1 fast path (V = 2) applies: KH = KW = 1, stride 1, no padding (A row m is A + m·lda), and
+// every byte offset of a batch member's A and weight plane fits 32 bits.
+inline bool t1_ok(const ConvArgs& a) {
+  const sp_conv_desc& d = a.d;
+  return d.KH == 1 && d.KW == 1 && d.stride == 1 && d.pad == 0 && d.Ho == d.H && d.Wo == d.W &&
+         a.M * d.lda * 4 < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
+}
+
+template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int V = 0>
 int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   if (a.d.Cin % BK || a.K % BK) {
     set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
@@ -306,10 +347,22 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   ConvArgs ab = a;
   ab.tiles_per_batch = (int32_t)per;
   dim3 grid((unsigned)tiles, 1, a.splits);
-  if (planes == 3)
+  if constexpr (V >= 1) {
+    // variant kernels: the 1×1 fast path where it applies, else the pair-split form
+    const bool t1 = t1_ok(a);
+    if (planes == 3 && t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
+    else if (planes == 3)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+    else if (t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
+    else
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+  } else if (planes == 3) {
     hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
-  else
+  } else {
     hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
+  }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -352,6 +405,13 @@ int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
     case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
     case 65: return launch_glds<8, 1, 1, 4, 2, 32, true>(a, planes, s);  // cfg 63 on 16x16x32 MFMAs
+    // variants (V >= 1: pair-split + 1×1 fast path) of the most-used tiles, cfg + 100 (A/B)
+    case 133: return launch_glds<4, 2, 2, 4, 2, 32, false, 1>(a, planes, s);
+    case 144: return launch_glds<4, 1, 2, 4, 2, 16, false, 1>(a, planes, s);
+    case 145: return launch_glds<2, 2, 2, 2, 2, 32, false, 1>(a, planes, s);
+    case 146: return launch_glds<2, 2, 2, 2, 2, 16, false, 1>(a, planes, s);
+    case 147: return launch_glds<2, 2, 2, 2, 2, 32, true, 1>(a, planes, s);
+    case 163: return launch_glds<8, 1, 1, 4, 2, 32, false, 1>(a, planes, s);
     default: return -2;
   }
 }

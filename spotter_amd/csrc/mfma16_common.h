@@ -84,6 +84,43 @@ __device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, b
   split8<PL>(x0, x1, out);
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Two fp32 → one packed bf16 pair (RNE): a single v_cvt_pk_bf16_f32.
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+// split8 written pair by pair so it compiles to the minimum VALU stream per 8 elements: 12
+// v_cvt_pk_bf16_f32, 8 + 8 unpacks (the low half of a pair is `u << 16`, the high half `u &
+// 0xffff0000`: bf16 → fp32 is exact) and 16 v_sub_f32 — 44 instructions, against ~60 for the
+// element-wise form (hipcc converts element by element, then repacks). Same RNE hi / mid / lo as split8.
+template <int PL>
+__device__ __forceinline__ void split_frag_pk(const float4& x0, const float4& x1, bf16x8* out) {
+  const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+  uint32_t H[4], M[4], L[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float a = v[2 * q], b = v[2 * q + 1];
+    const uint32_t h = cvt_pk_bf16(a, b);
+    H[q] = h;
+    if constexpr (PL == 3) {
+      const float ra = a - __builtin_bit_cast(float, h << 16);
+      const float rb = b - __builtin_bit_cast(float, h & 0xffff0000u);
+      const uint32_t m = cvt_pk_bf16(ra, rb);
+      M[q] = m;
+      L[q] = cvt_pk_bf16(ra - __builtin_bit_cast(float, m << 16), rb - __builtin_bit_cast(float, m & 0xffff0000u));
+    }
+  }
+  out[0] = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
+  if constexpr (PL == 3) {
+    out[1] = __builtin_bit_cast(bf16x8, make_uint4(M[0], M[1], M[2], M[3]));
+    out[2] = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
+  }
+}
+
 // s_waitcnt vmcnt(n) with expcnt / lgkmcnt left open (gfx9 encoding; n < 64), fenced for the
 // compiler so no LDS access moves across it.
 template <int N>
@@ -111,6 +148,18 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(gsrc), "s"(lds_base)
+      : "memory");
+}
+
+// The same DMA with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset
+// (global_load_lds_dwordx4 vOff, s[base]): advancing a k-step is then one scalar add on the base
+// instead of a 64-bit VALU add + bounds select per piece (the 1×1 / batched-GEMM fast path).
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds_base)
       : "memory");
 }
 

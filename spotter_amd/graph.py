@@ -29,7 +29,9 @@ class GraphRunner:
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            # thread_local: request threads may keep launching (processor uploads) while the batcher
+            # thread captures; their work is on other streams and is not part of this graph
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 self.logits, self.boxes = engine.forward(self.x, microbatches=1)
         finally:
             engine._ws, engine._outs = saved

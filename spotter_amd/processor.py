@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import json
 import os
+import threading
 
 import numpy as np
 import torch
@@ -81,12 +82,18 @@ class SpotterImageProcessor:
         self.device = device
         self._stage = None  # pinned host staging buffer, reused across calls
         self._stage_done = None  # event after the last H2D copy out of it
+        self._stage_lock = threading.Lock()  # request threads may share one processor
 
     def __getstate__(self):
         st = self.__dict__.copy()
         st["_stage"] = None
         st["_stage_done"] = None
+        st["_stage_lock"] = None
         return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self._stage_lock = threading.Lock()
 
     @classmethod
     def from_pretrained(cls, path_or_name, **kwargs):
@@ -117,20 +124,21 @@ class SpotterImageProcessor:
         for n in sizes:  # 256-B aligned slots (the same-size kernel reads 4-byte words)
             offs.append(total)
             total += (n + 255) & ~255
-        if self._stage_done is not None:
-            self._stage_done.synchronize()
-        if self._stage is None or self._stage.numel() < total:
-            self._stage = torch.empty((max(total, 1 << 20),), dtype=torch.uint8, pin_memory=True)
         dst = torch.empty((total,), dtype=torch.uint8, device=dev)
-        host = self._stage.numpy()
-        ups = []
-        for a, n, off in zip(arrs, sizes, offs):
-            host[off:off + n] = a.reshape(-1)
-            ups.append(dst[off:off + n].view(a.shape))
-        dst.copy_(self._stage[:total], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        self._stage_done = ev
+        with self._stage_lock:  # fill → async copy → event, one caller at a time
+            if self._stage_done is not None:
+                self._stage_done.synchronize()
+            if self._stage is None or self._stage.numel() < total:
+                self._stage = torch.empty((max(total, 1 << 20),), dtype=torch.uint8, pin_memory=True)
+            host = self._stage.numpy()
+            ups = []
+            for a, n, off in zip(arrs, sizes, offs):
+                host[off:off + n] = a.reshape(-1)
+                ups.append(dst[off:off + n].view(a.shape))
+            dst.copy_(self._stage[:total], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._stage_done = ev
         return ups
 
     def _dev(self):

@@ -29,3 +29,15 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Write the observed parity margins of the golden tests (tests/margins.py), if any ran."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    if here not in sys.path:
+        sys.path.insert(0, here)
+    import margins
+
+    path = margins.write()
+    if path:
+        print(f"\nparity margins -> {path}")

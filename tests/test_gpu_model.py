@@ -7,6 +7,7 @@ encoder top-k anchor index (the decoder is permutation-equivariant over
 queries, so only the selected *set* matters, SURVEY.md §7 "Hard parts").
 """
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import margins  # noqa: E402
 SCORE_TOL = 1e-3
 BOX_TOL_PX = 0.5
 
@@ -31,24 +34,40 @@ def load_images(g):
     return [Image.fromarray(golden_source(int(s), int(h), int(w), pic)) for s, (h, w) in zip(g["seeds"], srcs)]
 
 
-def match_detections(got, exp_scores, exp_labels, exp_boxes):
-    """Every expected detection has a partner with the same label, score ±1e-3, box ±0.5 px."""
+def match_detections(got, exp_scores, exp_labels, exp_boxes, threshold=0.5, case=None):
+    """Every expected detection has a partner with the same label, score ±1e-3, box ±0.5 px. The bar's
+    own tolerance band at the threshold is honoured: a detection whose score is within 1e-3 of the
+    threshold may be present on one side only (HF 0.5004 vs ours 0.4997 is within the score bar).
+    The worst matched |Δscore| / box Δpx and the border detections are recorded (tests/margins.py)."""
     gs, gl, gb = got["scores"].numpy(), got["labels"].numpy(), got["boxes"].numpy()
-    assert len(gs) == len(exp_scores), f"{len(gs)} detections vs {len(exp_scores)} expected"
+    exp_scores = np.asarray(exp_scores)
+    border_e = np.abs(exp_scores - threshold) <= SCORE_TOL
+    border_g = np.abs(gs - threshold) <= SCORE_TOL
     used = set()
-    for s, l, b in zip(exp_scores, exp_labels, exp_boxes):
+    ds = db = 0.0
+    for s, l, b, brd in zip(exp_scores, exp_labels, exp_boxes, border_e):
         cand = [i for i in range(len(gs)) if i not in used and gl[i] == l
                 and abs(gs[i] - s) <= SCORE_TOL and np.abs(gb[i] - b).max() <= BOX_TOL_PX]
-        assert cand, f"no match for label {l} score {s:.5f} box {b}"
-        used.add(cand[0])
+        if not cand:
+            assert brd, f"no match for label {l} score {s:.5f} box {b}"
+            continue
+        i = min(cand, key=lambda i: max(abs(gs[i] - s) / SCORE_TOL, np.abs(gb[i] - b).max() / BOX_TOL_PX))
+        used.add(i)
+        ds = max(ds, abs(float(gs[i]) - float(s)))
+        db = max(db, float(np.abs(gb[i] - b).max()))
+    extra = [i for i in range(len(gs)) if i not in used]
+    assert all(border_g[i] for i in extra), f"{len(extra)} detections without an expected partner"
+    margins.record(case, det_dscore=ds, det_dbox_px=db, detections_n=len(exp_scores),
+                   border_unmatched_n=len(exp_scores) - len(used) + len(extra),
+                   near_threshold_n=int((np.abs(exp_scores - threshold) <= 0.05).sum()))
 
 
-def check_image(g, i, det, logits, boxes, topk):
+def check_image(g, i, det, logits, boxes, topk, case=None):
     """Image `i` of golden set g: detections at the parity bar, then every decoder query's logits /
-    box aligned by its encoder top-k anchor (>= 298 of the 300 anchors shared)."""
+    box aligned by its encoder top-k anchor (>= 298 of the 300 anchors shared). Margins → `case`."""
     starts = np.concatenate([[0], np.cumsum(g["det_counts"])]).astype(int)
     a, b = starts[i], starts[i + 1]
-    match_detections(det, g["det_scores"][a:b], g["det_labels"][a:b], g["det_boxes"][a:b])
+    match_detections(det, g["det_scores"][a:b], g["det_labels"][a:b], g["det_boxes"][a:b], case=case)
     th, tw = g["target_sizes"][i]
     exp_topk = g["enc_topk_ind"][i]
     common = set(topk.tolist()) & set(exp_topk.tolist())
@@ -57,9 +76,12 @@ def check_image(g, i, det, logits, boxes, topk):
     rows_e = [j for j, q in enumerate(exp_topk.tolist()) if q in common]
     rows_g = [pos_g[exp_topk[j]] for j in rows_e]
     sig = lambda x: 1 / (1 + np.exp(-x.astype(np.float64)))
-    assert np.abs(sig(logits[rows_g]) - sig(g["logits"][i][rows_e])).max() <= SCORE_TOL
+    dsig = np.abs(sig(logits[rows_g]) - sig(g["logits"][i][rows_e])).max()
     scale = np.array([tw, th, tw, th], np.float64)
-    assert (np.abs(boxes[rows_g] - g["pred_boxes"][i][rows_e]) * scale).max() <= BOX_TOL_PX
+    dbox = (np.abs(boxes[rows_g] - g["pred_boxes"][i][rows_e]) * scale).max()
+    margins.record(case, dsigma=dsig, dbox_px=dbox, anchors_shared_min=len(common), images_n=1)
+    assert dsig <= SCORE_TOL, dsig
+    assert dbox <= BOX_TOL_PX, dbox
 
 
 def run_case(preset, tag=None, precision="fp32", model=None):
@@ -80,7 +102,8 @@ def run_case(preset, tag=None, precision="fp32", model=None):
         th, tw = g["target_sizes"][i]
         det = proc.post_process_object_detection(out, target_sizes=torch.tensor([[th, tw]]), threshold=0.5)[0]
         topk = model.engine._ws["topk"][:300].cpu().numpy()
-        check_image(g, i, det, out.logits[0].cpu().numpy(), out.pred_boxes[0].cpu().numpy(), topk)
+        check_image(g, i, det, out.logits[0].cpu().numpy(), out.pred_boxes[0].cpu().numpy(), topk,
+                    case=f"{tag or preset + '_640'}_{precision}_bs1")
     return model
 
 
@@ -121,7 +144,7 @@ def test_r101vd_bs32_winograd_f23_matches_hf_goldens():
     F(4x4,3x3): the same parity bar per image."""
     model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, "fp32", wino_m=2)
     for b in range(32):
-        check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b])
+        check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b], case="r101vd_640_fp32_bs32_wino_f23")
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp32-mfma"])
@@ -132,7 +155,7 @@ def test_r101vd_bs32_headline_config_matches_hf_goldens(precision):
     model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, precision)
     assert logits.shape == (32, 300, 80)
     for b in range(32):
-        check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b])
+        check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b], case=f"r101vd_640_{precision}_bs32")
 
 
 def test_r18vd_bf16_bs256_config_c3():
@@ -147,6 +170,7 @@ def test_r18vd_bf16_bs256_config_c3():
     model, g, dets, logits, boxes, topk = run_tiled_batch("r18vd", 64, "bf16")
     assert logits.shape == (256, 300, 80)
     st = match_stats(dets, g)
+    margins.record("r18vd_640_bf16_bs256", recall_vs_fp32_min=st["recall_vs_fp32"], p95_dscore=st["p95_dscore"])
     assert st["recall_vs_fp32"] >= 0.8 and st["p95_dscore"] <= 0.05, st
     # every copy of an image inside the batch is bit-identical (rows never interact)
     for b in range(4, 256):
@@ -163,6 +187,48 @@ def test_r18vd_bf16_bs256_config_c3():
         # itself (measured p95 0.007, max 0.017), not at fp32 reassociation size
         d = np.abs(s1 - sb)
         assert np.percentile(d, 95) <= 0.02 and d.max() <= 0.06, (i, np.percentile(d, 95), d.max())
+
+
+# bf16 bar of the R101vd replica workload (C4), against the HF fp32 goldens: recall of the fp32 detections
+# at IoU 0.5 (bf16 detections at the serving threshold), p95 |Δscore| of the matched pairs, and the COCO-style
+# AP of the bf16 ranked candidates with the fp32 detections as ground truth (tools/bf16_delta.py). Values
+# measured on the round-3 tree are in profiles/r3/bf16_delta.json; the bars leave room for tile / split-K
+# changes (each reorders fp32 sums that feed bf16 roundings) but not for a broken path.
+BF16_R101_RECALL = 0.85     # measured 0.906 (2760 of 3048 fp32 detections)
+BF16_R101_P95_DSCORE = 0.08  # measured 0.052 (p50 0.033)
+BF16_R101_MAP = 0.85        # measured 0.916 (AP50 0.926)
+
+
+def test_r101vd_bf16_bs32_config_c4_replica():
+    """C4's per-replica workload: R101vd bf16 at batch 32 on one GPU (one Serve replica per MI355X;
+    serve.py:203, MODEL_NAME PekingU/rtdetr_v2_r101vd). The 4 r101vd goldens tiled ×8 through
+    Engine(precision="bf16") in one batch, at the stated bf16 bar against the HF fp32 goldens; every copy of
+    an image in the batch is bit-identical; a bs1 call of the same engine gives each image what the batch
+    gives, to the size of the bf16 delta itself (split-K at bs1 reorders the fp32 sums that feed bf16)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from spotter_amd import SpotterImageProcessor
+    from tools.bf16_delta import ap_vs_fp32, match_stats
+    from types import SimpleNamespace
+
+    model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, "bf16")
+    assert logits.shape == (32, 300, 80)
+    proc = SpotterImageProcessor()
+    st = match_stats(dets, g)
+    ap = ap_vs_fp32(SimpleNamespace(logits=torch.from_numpy(logits).cuda(), pred_boxes=torch.from_numpy(boxes).cuda()),
+                    g, proc)
+    margins.record("r101vd_640_bf16_bs32", recall_vs_fp32_min=st["recall_vs_fp32"], p95_dscore=st["p95_dscore"],
+                   map_vs_fp32_min=ap["map"], ap50_vs_fp32_min=ap["ap50"])
+    assert st["recall_vs_fp32"] >= BF16_R101_RECALL and st["p95_dscore"] <= BF16_R101_P95_DSCORE, st
+    assert ap["map"] >= BF16_R101_MAP, ap
+    for b in range(4, 32):
+        assert np.array_equal(logits[b], logits[b % 4]), b
+    sig = lambda x: 1 / (1 + np.exp(-x.astype(np.float64)))
+    for i, img in enumerate(load_images(g)):
+        with torch.no_grad():
+            o1 = model(**proc(images=img))
+        d = np.abs(np.sort(sig(o1.logits[0].cpu().numpy()).max(-1)) - np.sort(sig(logits[i]).max(-1)))
+        margins.record("r101vd_640_bf16_bs1_vs_bs32", p95_dscore=np.percentile(d, 95), max_dscore=d.max())
+        assert np.percentile(d, 95) <= 0.03 and d.max() <= 0.1, (i, np.percentile(d, 95), d.max())
 
 
 # "fp32": GEMMs as 3-way bf16 splits (SP_PREC_F32X3, the default path); "fp32-mfma": v_mfma_f32_32x32x2_f32.
@@ -189,7 +255,8 @@ def test_r101vd_1280_mixed_resolution_matches_hf_goldens():
     off = 0
     for i, det in enumerate(dets):
         n = int(g["det_counts"][i])
-        match_detections(det, g["det_scores"][off:off + n], g["det_labels"][off:off + n], g["det_boxes"][off:off + n])
+        match_detections(det, g["det_scores"][off:off + n], g["det_labels"][off:off + n], g["det_boxes"][off:off + n],
+                         case="r101vd_1280_fp32_mixed_batch")
         off += n
 
 

@@ -614,3 +614,47 @@ def test_tile_table_entries_can_run_their_configuration():
     assert len(rows) > 50
     bad = [r for r in rows if r[0] and r[5] and not runnable(r[6], r[2] // (r[3] * r[3]), r[1])]
     assert bad == []
+
+
+def _ap():
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import coco_ap
+
+    return coco_ap
+
+
+def test_coco_ap_hand_built_cases():
+    """tools/coco_ap.py (COCOeval bbox restated: greedy best-IoU matching, 101-point interpolated precision,
+    IoU 0.50:0.95) on cases whose AP is known by hand."""
+    ap = _ap().average_precision
+    g = {"boxes": np.array([[0, 0, 10, 10], [20, 20, 30, 30]], float), "labels": np.array([1, 1])}
+    perfect = dict(g, scores=np.array([0.9, 0.8]))
+    assert ap([perfect], [g])["map"] == 1.0
+    # hit (0.9), false positive (0.8), hit (0.7): precision 1 up to recall 0.5, then 2/3 (envelope)
+    d = {"boxes": np.array([[0, 0, 10, 10], [50, 50, 60, 60], [20, 20, 30, 30]], float),
+         "labels": np.array([1, 1, 1]), "scores": np.array([0.9, 0.8, 0.7])}
+    assert abs(ap([d], [g])["map"] - (51 * 1.0 + 50 * (2 / 3)) / 101) < 1e-12
+    # one detection with IoU 0.6 against its only GT: a hit at IoU 0.50, 0.55, 0.60 only → AP 0.3
+    one = {"boxes": np.array([[0, 0, 10, 10]], float), "labels": np.array([3])}
+    shifted = {"boxes": np.array([[0, 0, 10, 6]], float), "labels": np.array([3]), "scores": np.array([0.5])}
+    assert abs(_ap().box_iou(shifted["boxes"], one["boxes"])[0, 0] - 0.6) < 1e-12
+    r = ap([shifted], [one])
+    assert abs(r["map"] - 0.3) < 1e-12 and r["ap50"] == 1.0 and r["ap75"] == 0.0
+    # a duplicate of a matched detection is a false positive; a wrong label is not a hit at all
+    dup = {"boxes": np.array([[0, 0, 10, 10]] * 2, float), "labels": np.array([3, 3]), "scores": np.array([0.9, 0.8])}
+    assert ap([dup], [one])["map"] == 1.0  # the FP comes after recall 1 was reached
+    dup2 = dict(dup, scores=np.array([0.8, 0.9]))
+    assert ap([dup2], [one])["map"] == 1.0
+    wrong = dict(dup, labels=np.array([4, 4]))
+    assert ap([wrong], [one])["map"] == 0.0
+    # two images, classes averaged: class 1 perfect, class 2 missed entirely → mAP 0.5
+    g2 = {"boxes": np.array([[0, 0, 5, 5]], float), "labels": np.array([2])}
+    none = {"boxes": np.zeros((0, 4)), "labels": np.zeros(0, int), "scores": np.zeros(0)}
+    r = ap([perfect, none], [g, g2])
+    assert r["per_class"] == {1: 1.0, 2: 0.0} and r["map"] == 0.5
+    # maxDets: only the top 100 detections per image count
+    many = {"boxes": np.array([[100, 100, 110, 110]] * 100 + [[0, 0, 10, 10]], float),
+            "labels": np.ones(101, int), "scores": np.concatenate([np.full(100, 0.9), [0.1]])}
+    assert ap([many], [{"boxes": one["boxes"], "labels": np.array([1])}])["map"] == 0.0

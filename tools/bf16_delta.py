@@ -1,8 +1,15 @@
 """bf16 variant vs the fp32 reference outputs (tests/golden): the accuracy delta we can state offline.
 
-COCO-val mAP needs the real checkpoint and COCO images (both unreachable offline), so the bf16 delta is
-reported as detection agreement with the HF fp32 goldens on the synthetic-weight model: matched
-detections (same label, IoU >= 0.5), max |Δscore| of matched pairs, and missed / extra detections.
+COCO-val mAP needs the real checkpoint and COCO images (both unreachable offline: "parity unpinned"),
+so the bf16 delta is reported against the HF fp32 goldens on the synthetic-weight model, two ways:
+
+* detection agreement at the serving threshold 0.5: matched detections (same label, IoU >= 0.5),
+  recall of the fp32 detections, |Δscore| of matched pairs, extra detections;
+* COCO-style AP (tools/coco_ap.py, IoU 0.50:0.95, 101-point) of the bf16 path's ranked candidates
+  (post-process threshold 0, the model's own 300 per image, maxDets 300) with the fp32 detections
+  above 0.5 taken as ground truth: AP 1.0 means bf16 reproduces fp32's detections exactly.
+
+    python tools/bf16_delta.py [bf16|bf16-all] [--reps 8] [--out profiles/r3/bf16_delta.json]
 """
 import json
 import os
@@ -57,7 +64,34 @@ def match_stats(dets, g):
     return tot
 
 
-def delta(preset, tag=None, precision="bf16"):
+def golden_gt(g, n):
+    """The fp32 golden detections (score > 0.5) of images 0..n-1 (image i ↔ golden i % count) as AP ground truth."""
+    starts = np.concatenate([[0], np.cumsum(g["det_counts"])]).astype(int)
+    out = []
+    for i in range(n):
+        gi = i % len(g["det_counts"])
+        a, b = starts[gi], starts[gi + 1]
+        out.append({"boxes": g["det_boxes"][a:b], "labels": g["det_labels"][a:b]})
+    return out
+
+
+def ap_vs_fp32(out, g, proc):
+    """COCO-style AP of a model output's ranked candidates (threshold 0: the 300 per image the
+    post-process keeps) against the fp32 golden detections; maxDets 300 (the model's own cap)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from coco_ap import average_precision
+
+    n = out.logits.shape[0]
+    tsz = torch.tensor(np.tile(g["target_sizes"], (n // len(g["det_counts"]) + 1, 1))[:n])
+    cand = proc.post_process_object_detection(out, target_sizes=tsz, threshold=0.0)
+    dets = [{k: v.numpy() for k, v in c.items()} for c in cand]
+    r = average_precision(dets, golden_gt(g, n), max_dets=300)
+    return {"map": r["map"], "ap50": r["ap50"], "ap75": r["ap75"]}
+
+
+def delta(preset, tag=None, precision="bf16", reps=1):
+    """The golden images (tiled `reps` times into one batch) through Engine(precision) → agreement
+    with the fp32 goldens at threshold 0.5 and the AP of the ranked candidates."""
     from tests.test_gpu_model import load_images
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
     from spotter_amd.config import PRESETS
@@ -68,16 +102,30 @@ def delta(preset, tag=None, precision="bf16"):
     model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)
     model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision)
     proc = SpotterImageProcessor(size={"height": size, "width": size})
-    dets = []
-    for i, img in enumerate(load_images(g)):
-        out = model(**proc(images=img))
-        th, tw = g["target_sizes"][i]
-        dets.append(proc.post_process_object_detection(out, target_sizes=torch.tensor([[th, tw]]), threshold=0.5)[0])
-    return match_stats(dets, g)
+    imgs = load_images(g) * reps
+    with torch.no_grad():
+        out = model(**proc(images=imgs))
+    tsz = torch.tensor(np.tile(g["target_sizes"], (reps, 1)))
+    dets = proc.post_process_object_detection(out, target_sizes=tsz, threshold=0.5)
+    st = match_stats(dets, g)
+    st["ap_vs_fp32"] = ap_vs_fp32(out, g, proc)
+    st["images"] = len(imgs)
+    return st
 
 
 if __name__ == "__main__":
-    prec = sys.argv[1] if len(sys.argv) > 1 else "bf16"
-    res = {p: delta(p, precision=prec) for p in ("r18vd", "r101vd")}
-    res["precision"] = prec
-    print(json.dumps({"metric": "bf16 variant detection delta vs HF fp32 goldens (synthetic weights)", **res}))
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("precision", nargs="?", default="bf16")
+    ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    res = {p: delta(p, precision=a.precision, reps=a.reps) for p in ("r18vd", "r101vd")}
+    res["precision"] = a.precision
+    line = json.dumps({"metric": "bf16 variant delta vs HF fp32 goldens (synthetic weights; COCO-val unpinned)",
+                       **res})
+    print(line)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        open(a.out, "w").write(line + "\n")
