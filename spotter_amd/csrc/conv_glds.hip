@@ -5,8 +5,29 @@
 #ifndef SP_ABLATE
 #define SP_ABLATE 0
 #endif
+// Diagnostic build only (-DSP_GLDS_STAMP): per workgroup (first 16384), wave 0 lane 0 records
+// s_memtime at kernel start, when the first k-stage is ready, after the main loop and after the
+// epilogue, plus HW_ID (CU / SIMD placement); read back with sp_debug_glds_stamps
+// (tools/microbench/glds_stamps.py). Not in the product build.
+#ifndef SP_GLDS_STAMP
+#define SP_GLDS_STAMP 0
+#endif
 
 namespace sp {
+
+#if SP_GLDS_STAMP
+__device__ unsigned long long g_glds_stamps[16384 * 6];
+#define GLDS_STAMP(k)                                                                                 \
+  do {                                                                                              \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_glds_stamps[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);                                                              \
+  } while (0)
+#else
+#define GLDS_STAMP(k) \
+  do {                \
+  } while (0)
+#endif
 
 namespace {
 
@@ -33,12 +54,14 @@ struct GldsCfg {
 
 // The LDS-DMA main loop of one output tile: k-tiles [kt0, kt1) of tile `wg` (N fastest) accumulated
 // into acc (acc4 for 16x16x32 MFMAs). The caller zeroes the accumulators and owns the epilogue.
-// V (variant): 0 = element-wise split, per-piece 64-bit addresses with tap walk and bounds selects;
-// 1 = pair-wise split (split_frag_pk: the minimum VALU stream); 2 = 1 + the 1×1 fast path (KH = KW = 1,
-// stride 1, no padding, A / weight byte offsets < 4 GiB): per-lane 32-bit offsets against SGPR bases
-// that advance by one scalar add per k-step (glds16s); rows past M / columns past Cout re-read the last
-// valid row / column (their outputs are masked in the epilogue) instead of a zero block.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 0>
+// V (variant): 1 = general implicit GEMM (per-piece 64-bit addresses, tap walk, padding selects);
+// 2 = the 1×1 fast path (KH = KW = 1, stride 1, no padding, A / weight byte offsets < 4 GiB): per-lane
+// 32-bit offsets against SGPR bases that advance by one scalar add per k-step (glds16s); rows past M /
+// columns past Cout re-read the last valid row / column (their outputs are masked in the epilogue)
+// instead of a zero block. Both split A pair-wise (split_frag_pk). Bit-identical outputs, measured
+// 1.02-1.09× over the previous form (element-wise split, general addressing everywhere) on the C2
+// shapes (profiles/r3/ab_glds_v2.jsonl, tools/ab_glds.py).
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1>
 __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
                                           f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
@@ -185,8 +208,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
         bf16x8 fa[PL];
-        if constexpr (V >= 1) split_frag_pk<PL>(x0, x1, fa);
-        else split_frag<PL>(x0, x1, fa);
+        split_frag_pk<PL>(x0, x1, fa);
 #pragma unroll
         for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
       }
@@ -219,8 +241,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
           for (int q = 0; q < PL; ++q) fa[q] = hh;
         }
 #else
-        if constexpr (V >= 1) split_frag_pk<PL>(x0, x1, fa);
-        else split_frag<PL>(x0, x1, fa);
+        split_frag_pk<PL>(x0, x1, fa);
 #endif
 #if SP_ABLATE == 3  // no MFMA: keep the operands alive
 #pragma unroll
@@ -247,6 +268,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     else if (NS >= 3 && ahead >= 1) wait_vmcnt<(NS >= 3 ? GLDS : 0)>();
     else wait_vmcnt<0>();
     raw_barrier();
+    if (kt == 0) GLDS_STAMP(1);
 #if SP_ABLATE == 1  // no DMA in the loop (compute on stale stages)
     if (false)
 #else
@@ -302,10 +324,11 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
                                     n0 + wn * TN * 32, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 0>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1>
 __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
   __shared__ uint4 smem[C::SMEM];
+  GLDS_STAMP(0);
   int wg = xcd_index(blockIdx.x, gridDim.x);
   // batched launch (Winograd components): member bi owns tiles [bi·tiles_per_batch, (bi+1)·…)
   const int bi = p.batch > 1 ? wg / p.tiles_per_batch : 0;
@@ -317,10 +340,22 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs 
   f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   glds_zero<TM, TN, M16>(acc, acc4);
   glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V>(p, smem, wg, bi, kt0, kt1, acc, acc4);
+  GLDS_STAMP(2);
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   ConvArgs q = p;
   q.d.C += (int64_t)bi * p.bs_c;
   glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(q, smem, wg, acc, acc4);
+#if SP_GLDS_STAMP
+  __syncthreads();
+  GLDS_STAMP(3);
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_glds_stamps[blockIdx.x * 6 + 4] = hw;
+    g_glds_stamps[blockIdx.x * 6 + 5] = xcc;
+  }
+#endif
 }
 
 // The 1×1 fast path (V = 2) applies: KH = KW = 1, stride 1, no padding (A row m is A + m·lda), and
@@ -331,7 +366,7 @@ inline bool t1_ok(const ConvArgs& a) {
          a.M * d.lda * 4 < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
 }
 
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int V = 0>
+template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
 int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   if (a.d.Cin % BK || a.K % BK) {
     set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
@@ -347,22 +382,16 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   ConvArgs ab = a;
   ab.tiles_per_batch = (int32_t)per;
   dim3 grid((unsigned)tiles, 1, a.splits);
-  if constexpr (V >= 1) {
-    // variant kernels: the 1×1 fast path where it applies, else the pair-split form
-    const bool t1 = t1_ok(a);
-    if (planes == 3 && t1)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
-    else if (planes == 3)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
-    else if (t1)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
-    else
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
-  } else if (planes == 3) {
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
-  } else {
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16>), grid, dim3(64 * WM * WN), 0, s, ab);
-  }
+  // the 1×1 fast path where it applies, else the general implicit GEMM
+  const bool t1 = t1_ok(a);
+  if (planes == 3 && t1)
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
+  else if (planes == 3)
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+  else if (t1)
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
+  else
+    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -405,15 +434,14 @@ int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
     case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
     case 65: return launch_glds<8, 1, 1, 4, 2, 32, true>(a, planes, s);  // cfg 63 on 16x16x32 MFMAs
-    // variants (V >= 1: pair-split + 1×1 fast path) of the most-used tiles, cfg + 100 (A/B)
-    case 133: return launch_glds<4, 2, 2, 4, 2, 32, false, 1>(a, planes, s);
-    case 144: return launch_glds<4, 1, 2, 4, 2, 16, false, 1>(a, planes, s);
-    case 145: return launch_glds<2, 2, 2, 2, 2, 32, false, 1>(a, planes, s);
-    case 146: return launch_glds<2, 2, 2, 2, 2, 16, false, 1>(a, planes, s);
-    case 147: return launch_glds<2, 2, 2, 2, 2, 32, true, 1>(a, planes, s);
-    case 163: return launch_glds<8, 1, 1, 4, 2, 32, false, 1>(a, planes, s);
     default: return -2;
   }
 }
 
 }  // namespace sp
+
+#if SP_GLDS_STAMP
+extern "C" int sp_debug_glds_stamps(void* dst) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(sp::g_glds_stamps), sizeof(sp::g_glds_stamps));
+}
+#endif

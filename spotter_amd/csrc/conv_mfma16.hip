@@ -211,7 +211,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
 #pragma unroll
     for (int i = 0; i < TA; ++i) {
       bf16x8 pv[PL];
-      split8<PL>(ra[i][0], ra[i][1], pv);
+      split_frag_pk<PL>(ra[i][0], ra[i][1], pv);
       const int row = (tid + NT * i) >> 2;
 #pragma unroll
       for (int pl = 0; pl < PL; ++pl) *reinterpret_cast<bf16x8*>(st + pl * PA + sw16(row, c)) = pv[pl];
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
       const int c0 = 4 * s + 2 * h;
       const float4 x0 = *reinterpret_cast<const float4*>(st + a_row[i] + (c0 ^ a_sz[i]));
       const float4 x1 = *reinterpret_cast<const float4*>(st + a_row[i] + ((c0 + 1) ^ a_sz[i]));
-      split8<PL>(x0, x1, fa[i]);
+      split_frag_pk<PL>(x0, x1, fa[i]);
     }
   };
   auto mma = [&](const bf16x8 (&fa)[TM][PL], const bf16x8 (&fb)[TN][PL]) {
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
         const int c0 = 4 * s + 2 * h;
         const float4 x0 = *reinterpret_cast<const float4*>(st + a_row[i] + (c0 ^ a_sz[i]));
         const float4 x1 = *reinterpret_cast<const float4*>(st + a_row[i] + ((c0 + 1) ^ a_sz[i]));
-        split8<PL>(x0, x1, fa[s][i]);
+        split_frag_pk<PL>(x0, x1, fa[s][i]);
       }
     }
   };
@@ -882,7 +882,7 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
                                                        __float_as_uint(x1.x), __float_as_uint(x1.y)));
     for (int q = 0; q < PL; ++q) out[q] = raw;
 #else
-    split8<PL>(x0, x1, out);
+    split_frag_pk<PL>(x0, x1, out);
 #endif
   };
   // B fragments double-buffered in registers: block j+1's ds_reads are issued before block j's
@@ -1179,7 +1179,7 @@ __global__ __launch_bounds__(512) void conv_x3p_kernel(const ConvArgs p, int nti
     const uint4* st = smem + buf * STAGE;
     const float4 x0 = *reinterpret_cast<const float4*>(st + apos0);
     const float4 x1 = *reinterpret_cast<const float4*>(st + apos1);
-    split8<PL>(x0, x1, out);
+    split_frag_pk<PL>(x0, x1, out);
   };
   auto mma = [&](int buf) {  // Cᵀ += W_j · Aᵀ for the 8 (TN) column blocks
     const uint4* st = smem + buf * STAGE + CA + bpos0;
@@ -1397,12 +1397,11 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 62 && cfg <= 65) ||
-       (cfg >= 133 && cfg <= 165)) && !a.d.A2) {
+  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 62 && cfg <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || (cfg > 75 && cfg < 133) || cfg > 165 || (cfg >= 73 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || cfg > 75 || (cfg >= 73 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

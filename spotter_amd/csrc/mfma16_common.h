@@ -79,11 +79,6 @@ __device__ __forceinline__ f32x4 mfma16x16_planes(const bf16x8* a, const bf16x8*
 // Padding taps, rows past M and columns past Cout read a 128-byte zero block instead.
 __device__ float4 g_zero_chunk[8];
 
-template <int PL>
-__device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, bf16x8* out) {
-  split8<PL>(x0, x1, out);
-}
-
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -121,6 +116,11 @@ __device__ __forceinline__ void split_frag_pk(const float4& x0, const float4& x1
   }
 }
 
+template <int PL>
+__device__ __forceinline__ void split_frag(const float4& x0, const float4& x1, bf16x8* out) {
+  split_frag_pk<PL>(x0, x1, out);
+}
+
 // s_waitcnt vmcnt(n) with expcnt / lgkmcnt left open (gfx9 encoding; n < 64), fenced for the
 // compiler so no LDS access moves across it.
 template <int N>
@@ -154,7 +154,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_base) {
 // The same DMA with a wave-uniform 64-bit base in SGPRs and a 32-bit per-lane byte offset
 // (global_load_lds_dwordx4 vOff, s[base]): advancing a k-step is then one scalar add on the base
 // instead of a 64-bit VALU add + bounds select per piece (the 1×1 / batched-GEMM fast path).
-__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, uint32_t lds_base) {
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* base, uint32_t lds_base) {
+  // the base IS wave-uniform, but hipcc cannot always prove it (it then hands the "s" operand a
+  // VGPR pair, which the assembler rejects): pin it to SGPRs
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  const uint64_t sbase = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"

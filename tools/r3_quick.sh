@@ -1,4 +1,6 @@
 set -euo pipefail
-OUT=gpurun_out/r3a; mkdir -p $OUT; export TMPDIR=/tmp
-timeout -k 10 420 python3 -u bench.py --no-cpu-baseline --latency-iters 0 --detail $OUT/detail.json > $OUT/bench.log 2>&1
-tail -1 $OUT/bench.log | cut -c1-400
+OUT=gpurun_out/r3d; mkdir -p $OUT; export TMPDIR=/tmp
+for b in 32 16 8; do
+  timeout -k 10 300 python3 -u bench.py --batch $b --steps 10 --no-cpu-baseline --latency-iters 0 --no-events > $OUT/bench_bs$b.log 2>&1
+  tail -1 $OUT/bench_bs$b.log | cut -c1-200
+done
