@@ -58,7 +58,7 @@ def parse():
                     help="bs1 /detect core requests for the p50 latency half of the metric (0 = skip)")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
     ap.add_argument("--stagger", type=int, default=1, help="block offset between micro-batch streams")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-mfma", "bf16", "bf16-all"],
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp32-mfma", "bf16", "bf16-convs", "bf16-all"],
                     help="GEMM operand precision: fp32 = fp32-accurate 3-way bf16 split GEMMs (SP_PREC_F32X3), "
                          "fp32-mfma = v_mfma_f32_32x32x2_f32 GEMMs; bf16 = the separately reported variant (C3/C4)")
     ap.add_argument("--winograd", default=None, choices=["off", "auto", "repvgg", "all"],
@@ -101,7 +101,7 @@ def union_ms(ivs):
 
 
 # the dominant kernel's operand mode per --precision: the split GEMM (x3) on the fp32 parity path
-DOMINANT_MODE = {"fp32": "x3", "fp32-mfma": "f32", "bf16": "bf16", "bf16-all": "bf16"}
+DOMINANT_MODE = {"fp32": "x3", "fp32-mfma": "f32", "bf16": "bf16", "bf16-convs": "bf16", "bf16-all": "bf16"}
 
 
 class KernelEventRecorder:

@@ -33,7 +33,11 @@ namespace {
 
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK>
 struct GldsCfg {
-  static_assert(BK == 32 || BK == 16, "k per stage");
+  // BK = 64 (4 k16 steps per barrier) is supported and was measured: 0.70-0.92x of the same wave tile at
+  // k32 for both operand modes (profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per
+  // CU), so no configuration uses it
+  static_assert(BK == 64 || BK == 32 || BK == 16, "k per stage");
+  static_assert(BK != 64 || 64 * WM * WN >= 256, "64-deep stages: the source swizzle needs >= 256 threads");
   static constexpr int NT = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
@@ -84,7 +88,9 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   // global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of the
   // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
   // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
-  const int ca = BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
+  // BK = 64: an A row is 16 chunks = one whole 256-byte bank row, swizzle row & 15
+  const int ca = BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
+               : BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
   const float* A = d.A + (int64_t)bi * p.bs_a;
   const uint16_t* Wt = d.Wt_bf16 + (int64_t)bi * p.bs_w;
   int a_iy0[GA], a_ix0[GA];
@@ -104,7 +110,9 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   }
   // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
   // (sw16), (row >> 3) & 1 at BK = 16.
-  const int cbk = BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
+  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
+  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
+                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
   const uint16_t* b_ptr[GB];
   bool b_ok[GB];
 #pragma unroll
@@ -220,7 +228,9 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int brow = wn * TN * 32 + j * 32 + r;
-        const int bpos = BK == 32 ? sw16(brow, 2 * s + h) : brow * 2 + (h ^ ((brow >> 3) & 1));
+        const int bpos = BK == 64   ? brow * 8 + ((2 * s + h) ^ ((brow >> 1) & 7))
+                         : BK == 32 ? sw16(brow, 2 * s + h)
+                                    : brow * 2 + (h ^ ((brow >> 3) & 1));
 #pragma unroll
         for (int pl = 0; pl < PL; ++pl)
           fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
@@ -228,7 +238,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * TM * 32 + i * 32 + r;
-        const int sz = BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
+        const int sz = BK == 64 ? row & 15 : BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
         const int c0 = 4 * s + 2 * h;
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
@@ -324,8 +334,10 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
                                     n0 + wn * TN * 32, lane);
 }
 
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1>
-__global__ __launch_bounds__(64 * WM * WN) void conv_glds_kernel(const ConvArgs p) {
+// OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained). Applied to the
+// 1×1 fast-path instantiations only (launch_glds): the general path's extra address registers spill.
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const ConvArgs p) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
   __shared__ uint4 smem[C::SMEM];
   GLDS_STAMP(0);
@@ -366,7 +378,7 @@ inline bool t1_ok(const ConvArgs& a) {
          a.M * d.lda * 4 < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
 }
 
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false>
+template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int OCC = 1>
 int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   if (a.d.Cin % BK || a.K % BK) {
     set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
@@ -379,19 +391,31 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
     set_error("sp_conv2d: %lld tiles exceed the grid (or split-K on a batched GEMM)", (long long)tiles);
     return -1;
   }
+  // a tile whose stages do not fit the 160 KB LDS for this operand mode is not instantiated
+  using C3 = GldsCfg<WM, WN, TM, TN, 3, NS, BK>;
+  using C1 = GldsCfg<WM, WN, TM, TN, 1, NS, BK>;
+  constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
+  if ((planes == 3 && !fit3) || (planes != 3 && !fit1)) {
+    set_error("sp_conv2d: tile stages exceed the LDS for %d operand plane(s)", planes);
+    return -1;
+  }
   ConvArgs ab = a;
   ab.tiles_per_batch = (int32_t)per;
   dim3 grid((unsigned)tiles, 1, a.splits);
   // the 1×1 fast path where it applies, else the general implicit GEMM
   const bool t1 = t1_ok(a);
-  if (planes == 3 && t1)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
-  else if (planes == 3)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
-  else if (t1)
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2>), grid, dim3(64 * WM * WN), 0, s, ab);
-  else
-    hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+  if constexpr (fit3) {
+    if (planes == 3 && t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC>), grid, dim3(64 * WM * WN), 0, s, ab);
+    else if (planes == 3)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+  }
+  if constexpr (fit1) {
+    if (planes != 3 && t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC>), grid, dim3(64 * WM * WN), 0, s, ab);
+    else if (planes != 3)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
+  }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
   return launch_splitk_reduce(a, s);
@@ -424,7 +448,11 @@ int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     case 43: return launch_glds<2, 2, 2, 2, 3, 32, true>(a, planes, s);  // cfg 11 on 16x16x32 MFMAs
     case 44: return launch_glds<4, 1, 2, 4, 2, 16>(a, planes, s);  // 256×128, 4 waves of 64×128, k16 × 2
     case 45: return launch_glds<2, 2, 2, 2, 2>(a, planes, s);      // 128×128, k32 × 2 stages
-    case 46: return launch_glds<2, 2, 2, 2, 2, 16>(a, planes, s);  // 128×128, k16 × 2 stages
+    // 128×128, k16 × 2 stages, registers for 4 waves per SIMD (four workgroups per CU): bit-identical,
+    // 1.02-1.09x over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
+    // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general
+    // path would spill: it keeps the unconstrained allocation)
+    case 46: return launch_glds<2, 2, 2, 2, 2, 16, false, 4>(a, planes, s);
     case 47: return launch_glds<2, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 45 on 16x16x32 MFMAs
     case 48: return launch_glds<2, 2, 2, 4, 2, 16>(a, planes, s);  // 128×256, 4 waves of 64×128, k16 × 2
     case 49: return launch_glds<4, 1, 2, 4, 2, 32, true>(a, planes, s);  // cfg 17 on 16x16x32 MFMAs

@@ -54,11 +54,17 @@ bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack 
 _X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256, True), (256, 512, True),
               (288, 256, True), (4, 256, False)}
 
+# The bf16 variant ("bf16") runs every conv and linear on bf16 operands; the stem's first conv stays on
+# the direct fp32 kernel (_direct_stem). Measured against the HF fp32 goldens (profiles/r3/bf16/, R101vd
+# bs32): recall 0.971, p95 |dscore| 0.012, AP 0.958 — closer than round 2's bf16 mode with x3 linears and
+# a bf16 stem (0.906 / 0.052 / 0.916: the bf16-rounded raw pixels of the stem conv were most of the error),
+# at 1.07x (C2) / 1.10x (C3) its speed. "bf16-convs" keeps the linears on the fp32-accurate split.
 PRECISIONS = {
     "fp32": ("x3", "x3"),
     "fp32-mfma": ("f32", "f32"),
-    "bf16": ("bf16", "x3"),
-    "bf16-all": ("bf16", "bf16"),
+    "bf16": ("bf16", "bf16"),
+    "bf16-convs": ("bf16", "x3"),
+    "bf16-all": ("bf16", "bf16"),  # round-2 name of "bf16"
 }
 
 
@@ -458,10 +464,11 @@ class Engine:
                           row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
     def _direct_stem(self) -> bool:
-        """The stem's first conv (Cin 3, K = 27) runs on the direct NCHW kernel (sp_stem_conv3x3s2_nchw)
-        in the fp32-weight modes; the bf16 variants keep it on the GEMM path with their rounding."""
+        """The stem's first conv (Cin 3, K = 27) runs on the direct NCHW kernel (sp_stem_conv3x3s2_nchw, fp32
+        weights, exact fmaf chains) in every precision mode: K = 27 gives a GEMM nothing to tile (the bf16
+        GEMM ran it at 20 TF/s, 2.3 ms of a C3 step, profiles/r3/bf16/), and fp32 here is only more exact."""
         c = self.stem[0]
-        return c.cin == 3 and c.k == 3 and c.cout in (32, 64) and c.w16 is None and self.act_bb in ("relu", None)
+        return c.cin == 3 and c.k == 3 and c.cout in (32, 64) and self.act_bb in ("relu", None)
 
     def backbone(self, pixel_values: torch.Tensor, B, H, W):
         """RTDetrResNetBackbone.forward RN:365-422 → [stage2, stage3, stage4] outputs (NHWC).

@@ -194,9 +194,9 @@ def test_r18vd_bf16_bs256_config_c3():
 # AP of the bf16 ranked candidates with the fp32 detections as ground truth (tools/bf16_delta.py). Values
 # measured on the round-3 tree are in profiles/r3/bf16_delta.json; the bars leave room for tile / split-K
 # changes (each reorders fp32 sums that feed bf16 roundings) but not for a broken path.
-BF16_R101_RECALL = 0.85     # measured 0.906 (2760 of 3048 fp32 detections)
-BF16_R101_P95_DSCORE = 0.08  # measured 0.052 (p50 0.033)
-BF16_R101_MAP = 0.85        # measured 0.916 (AP50 0.926)
+BF16_R101_RECALL = 0.92     # measured 0.971 (2960 of 3048 fp32 detections)
+BF16_R101_P95_DSCORE = 0.04  # measured 0.012 (p50 0.004)
+BF16_R101_MAP = 0.90        # measured 0.958 (AP50 0.959)
 
 
 def test_r101vd_bf16_bs32_config_c4_replica():

@@ -1,13 +1,14 @@
-"""A/B of the split-GEMM LDS-DMA kernel variants (conv_glds.hip V = 1 / 2, configurations cfg + 100)
-against their V = 0 originals, in ONE process with interleaved rounds (guide §5.4 rule 24).
+"""A/B of two LDS-DMA GEMM tile configurations (conv_glds.hip) in ONE process with interleaved rounds
+(guide §5.4 rule 24): kernel variants kept side by side during development, or two tiles.
 
-    python tools/ab_glds.py [--pairs 46:146,44:144] [--rounds 5] [--reps 10] [--out ab.jsonl]
+    python tools/ab_glds.py [--pairs 45:52,46:146] [--planes 3|1] [--rounds 5] [--reps 10] [--out ab.jsonl]
 
-1. Correctness: every variant must give BIT-IDENTICAL outputs to its original (same products, same
-   summation order) on 1×1 convs with ragged M / Cout edges and residual epilogues, and through the
-   batched Winograd component GEMMs.
-2. Timing: per shape, the original and the variant alternate for --rounds rounds of --reps launches;
-   the median ms of each is reported with the TFLOP/s (fp32-equivalent, 2·M·N·K).
+1. Correctness (unless --no-check): both configurations of a pair must give BIT-IDENTICAL outputs — true
+   whenever they share the wave tile and MFMA shape (same products, same k16 summation order; the stage
+   depth only changes when operands arrive) — on 1×1 convs with ragged M / Cout edges and residual
+   epilogues, and through the batched Winograd component GEMMs.
+2. Timing: per shape the two configurations alternate for --rounds rounds of --reps launches; the median
+   ms of each is reported with the TFLOP/s (fp32-equivalent, 2·M·N·K).
 """
 from __future__ import annotations
 
@@ -38,6 +39,9 @@ SHAPES = [
 EDGES = [(1, 1, 1000, 256, 192, True, "relu"), (3, 7, 9, 128, 320, False, None), (1, 1, 77, 512, 128, True, None)]
 
 
+PLANES = 3  # 3 = the fp32-accurate split (x3), 1 = the bf16 operand mode (--planes 1)
+
+
 def make(dev, shape, seed=0):
     g = torch.Generator(device=dev).manual_seed(seed)
     n, h, w, cin, cout = shape[:5]
@@ -52,11 +56,14 @@ def make(dev, shape, seed=0):
     kw = {}
     if wino:
         u = ops.winograd_weights_host(wt.view(cout, 3, 3, cin).cpu().numpy(), 4)
-        planes = torch.from_numpy(ops.split_bf16x3_host(u)).to(dev)
+        planes = (torch.from_numpy(ops.split_bf16x3_host(u)).to(dev) if PLANES == 3 else
+                  torch.from_numpy(ops.bf16_bits(u).reshape(1, -1).view("int16")).to(dev))
         work = torch.empty(36 * (n * ((h + 3) // 4) * ((w + 3) // 4)) * (cin + cout), device=dev)
         kw["wino"] = (planes, work, 4)
-    else:
+    elif PLANES == 3:
         kw["wt_planes"] = ops.split_bf16x3(wt)
+    else:
+        kw["wt16"] = torch.from_numpy(ops.bf16_bits(wt.cpu().numpy()).view("int16")).to(dev)
     act = None if wino else shape[6]
 
     def run():
@@ -87,7 +94,11 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--shapes", default=None)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--planes", type=int, default=3, choices=[1, 3])
+    ap.add_argument("--no-check", action="store_true", help="skip the bit-identity check (pairs of different tiles)")
     a = ap.parse_args()
+    global PLANES
+    PLANES = a.planes
     dev = torch.device("cuda", 0)
     pairs = [tuple(p.split(":")) for p in a.pairs.split(",")]
     lines = []
@@ -97,7 +108,7 @@ def main():
         lines.append(d)
 
     # 1. bit-identical outputs
-    for shape in EDGES + SHAPES[:1] + SHAPES[6:7]:
+    for shape in ([] if a.no_check else EDGES + SHAPES[:1] + SHAPES[6:7]):
         run, out, _ = make(dev, shape)
         for c0, c1 in pairs:
             res = []
@@ -116,7 +127,7 @@ def main():
                 emit({"check": list(shape), "pair": [c0, c1], "skipped": [r for r in res if isinstance(r, str)]})
                 continue
             same = torch.equal(res[0], res[1]) and not torch.isnan(res[1]).any().item()
-            emit({"check": list(shape), "pair": [c0, c1], "bit_identical": bool(same)})
+            emit({"check": list(shape), "pair": [c0, c1], "planes": PLANES, "bit_identical": bool(same)})
             if not same:
                 raise SystemExit(f"variant {c1} differs from {c0} on {shape}")
     # 2. interleaved timing
@@ -140,7 +151,7 @@ def main():
             if not ok or not t[c0] or not t[c1]:
                 continue
             m0, m1 = statistics.median(t[c0]), statistics.median(t[c1])
-            emit({"shape": list(shape), "pair": [c0, c1], "ms": [round(m0, 4), round(m1, 4)],
+            emit({"shape": list(shape), "pair": [c0, c1], "planes": PLANES, "ms": [round(m0, 4), round(m1, 4)],
                   "tflops": [round(flops / m0 / 1e9, 1), round(flops / m1 / 1e9, 1)], "speedup": round(m0 / m1, 3)})
     if a.out:
         with open(a.out, "w") as f:
