@@ -29,7 +29,10 @@ if os.environ.get("SP_TUNING_BUILD") == "1":
 
 
 def sources():
-    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    # the heavy template units first, so the parallel build ends with the short ones
+    heavy = ("conv_glds_p", "conv_mfma16", "conv_gemm")
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    return sorted(srcs, key=lambda p: not os.path.basename(p).startswith(heavy))
 
 
 def _deps_mtime():

@@ -1,469 +1,50 @@
-// LDS-DMA implicit-GEMM kernels on bf16-operand MFMA (x3 split / bf16): the tile
-// configurations 11-64 of launch_mfma16 (conv_mfma16.hip).
-#include "mfma16_common.h"
-
-#ifndef SP_ABLATE
-#define SP_ABLATE 0
-#endif
-// Diagnostic build only (-DSP_GLDS_STAMP): per workgroup (first 16384), wave 0 lane 0 records
-// s_memtime at kernel start, when the first k-stage is ready, after the main loop and after the
-// epilogue, plus HW_ID (CU / SIMD placement); read back with sp_debug_glds_stamps
-// (tools/microbench/glds_stamps.py). Not in the product build.
-#ifndef SP_GLDS_STAMP
-#define SP_GLDS_STAMP 0
-#endif
+// LDS-DMA implicit-GEMM kernels on bf16-operand MFMA (x3 split / bf16): the dispatcher of the tile
+// configurations 11-65 of launch_mfma16 (conv_mfma16.hip). The kernels live in conv_glds.h and are
+// instantiated across conv_glds_p<k>.hip; a diagnostic build (-DSP_GLDS_STAMP, tools/build_diag.sh)
+// instantiates them all here instead.
+#include "conv_glds.h"
 
 namespace sp {
 
 #if SP_GLDS_STAMP
-__device__ unsigned long long g_glds_stamps[16384 * 6];
-#define GLDS_STAMP(k)                                                                                 \
-  do {                                                                                              \
-    __builtin_amdgcn_sched_barrier(0);                                                              \
-    if (threadIdx.x == 0 && blockIdx.x < 16384) g_glds_stamps[blockIdx.x * 6 + (k)] = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);                                                              \
-  } while (0)
-#else
-#define GLDS_STAMP(k) \
-  do {                \
-  } while (0)
-#endif
-
 namespace {
-
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK>
-struct GldsCfg {
-  // BK = 64 (4 k16 steps per barrier) is supported and was measured: 0.70-0.92x of the same wave tile at
-  // k32 for both operand modes (profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per
-  // CU), so no configuration uses it
-  static_assert(BK == 64 || BK == 32 || BK == 16, "k per stage");
-  static_assert(BK != 64 || 64 * WM * WN >= 256, "64-deep stages: the source swizzle needs >= 256 threads");
-  static constexpr int NT = 64 * WM * WN;
-  static constexpr int BM = 32 * TM * WM;
-  static constexpr int BN = 32 * TN * WN;
-  static constexpr int RA = BK / 4;  // 16-byte chunks per fp32 A row (8 at BK = 32, 4 at BK = 16)
-  static constexpr int RB = BK / 8;  // 16-byte chunks per bf16 B row (4 / 2)
-  static constexpr int CA = BM * RA;  // 16-byte chunks of the fp32 A tile
-  static constexpr int CB = BN * RB;  // 16-byte chunks of one bf16 B plane
-  static constexpr int GA = CA / NT;
-  static constexpr int GB = CB / NT;
-  static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
-  static constexpr int GLDS = GA + PL * GB;  // DMA instructions per thread per stage
-  static constexpr int STAGE = CA + PL * CB;
-  static constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
-  static constexpr int EPI = WM * WN * NB * 32 * TN * 32 / 4;
-  static constexpr int SMEM = NS * STAGE > EPI ? NS * STAGE : EPI;
-  static_assert(NS >= 2 && NS <= 6, "stages");
-};
-
-// The LDS-DMA main loop of one output tile: k-tiles [kt0, kt1) of tile `wg` (N fastest) accumulated
-// into acc (acc4 for 16x16x32 MFMAs). The caller zeroes the accumulators and owns the epilogue.
-// V (variant): 1 = general implicit GEMM (per-piece 64-bit addresses, tap walk, padding selects);
-// 2 = the 1×1 fast path (KH = KW = 1, stride 1, no padding, A / weight byte offsets < 4 GiB): per-lane
-// 32-bit offsets against SGPR bases that advance by one scalar add per k-step (glds16s); rows past M /
-// columns past Cout re-read the last valid row / column (their outputs are masked in the epilogue)
-// instead of a zero block. Both split A pair-wise (split_frag_pk). Bit-identical outputs, measured
-// 1.02-1.09× over the previous form (element-wise split, general addressing everywhere) on the C2
-// shapes (profiles/r3/ab_glds_v2.jsonl, tools/ab_glds.py).
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1>
-__device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
-                                          f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
-  static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
-  constexpr int NT = C::NT, RA = C::RA, RB = C::RB, CA = C::CA, CB = C::CB, GA = C::GA, GB = C::GB;
-  constexpr int GLDS = C::GLDS, STAGE = C::STAGE, BM = C::BM, BN = C::BN;
-
-  const sp_conv_desc& d = p.d;
-  const int64_t wps = d.wt_plane_stride;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6;
-  const int lane = tid & 63;
-
-  const int tilesN = (d.Cout + BN - 1) / BN;
-  const int mt = wg / tilesN;
-  const int n0 = (wg - mt * tilesN) * BN;
-  const int64_t m0 = (int64_t)mt * BM;
-
-  // A pieces: piece j of this thread covers tile row (j·NT + tid) / RA, LDS position tid % RA,
-  // global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of the
-  // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
-  // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
-  // BK = 64: an A row is 16 chunks = one whole 256-byte bank row, swizzle row & 15
-  const int ca = BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
-               : BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
-  const float* A = d.A + (int64_t)bi * p.bs_a;
-  const uint16_t* Wt = d.Wt_bf16 + (int64_t)bi * p.bs_w;
-  int a_iy0[GA], a_ix0[GA];
-  const float* a_ptr[GA];
-#pragma unroll
-  for (int j = 0; j < GA; ++j) {
-    const int64_t m = m0 + (j * NT + tid) / RA;
-    const bool ok = m < p.M;
-    const int64_t mm = ok ? m : 0;
-    const int b = (int)(mm / p.HoWo);
-    const int rem = (int)(mm - (int64_t)b * p.HoWo);
-    const int oy = rem / d.Wo;
-    const int ox = rem - oy * d.Wo;
-    a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
-    a_ix0[j] = ox * d.stride - d.pad;
-    a_ptr[j] = A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
-  }
-  // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
-  // (sw16), (row >> 3) & 1 at BK = 16.
-  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
-  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
-                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
-  const uint16_t* b_ptr[GB];
-  bool b_ok[GB];
-#pragma unroll
-  for (int j = 0; j < GB; ++j) {
-    const int n = n0 + (j * NT + tid) / RB;
-    b_ok[j] = n < d.Cout;
-    b_ptr[j] = Wt + (int64_t)(b_ok[j] ? n : 0) * p.K + cbk * 8;
-  }
-  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
-  // V == 2: byte offsets of this lane's A rows / B rows against the operand bases
-  uint32_t a_off[V == 2 ? GA : 1], b_off[V == 2 ? GB : 1];
-  if constexpr (V == 2) {
-#pragma unroll
-    for (int j = 0; j < GA; ++j) {
-      const int64_t m = m0 + (j * NT + tid) / RA;
-      a_off[j] = (uint32_t)(((m < p.M ? m : p.M - 1) * d.lda + ca * 4) * 4);
-    }
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-      const int n = n0 + (j * NT + tid) / RB;
-      b_off[j] = (uint32_t)(((int64_t)(n < d.Cout ? n : d.Cout - 1) * p.K + cbk * 8) * 2);
-    }
-  }
-
-  int s_kh = 0, s_kw = 0, s_c0 = 0;
-  const int nk = kt1 - kt0;
-  {
-    const int k0 = kt0 * BK;
-    const int tap = k0 / d.Cin;
-    s_c0 = k0 - tap * d.Cin;
-    s_kh = tap / d.KW;
-    s_kw = tap - s_kh * d.KW;
-  }
-
-  // Issue the DMA pieces of k-tile kt into stage buffer `buf`, then advance the tap walk.
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)smem;
-  const uint32_t wave_off = (uint32_t)__builtin_amdgcn_readfirstlane(wave * 64 * 16);
-  auto issue = [&](int kt, int buf) {
-    const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
-    if constexpr (V == 2) {
-      const float* ab = A + (int64_t)kt * BK;
-#pragma unroll
-      for (int j = 0; j < GA; ++j) glds16s(a_off[j], ab, st + j * NT * 16);
-#pragma unroll
-      for (int pl = 0; pl < PL; ++pl) {
-        const uint16_t* bb = Wt + pl * wps + (int64_t)kt * BK;
-#pragma unroll
-        for (int j = 0; j < GB; ++j) glds16s(b_off[j], bb, st + (CA + pl * CB + j * NT) * 16);
-      }
-      return;
-    }
-    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
-#pragma unroll
-    for (int j = 0; j < GA; ++j) {
-      const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
-      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
-      glds16(src, st + j * NT * 16);
-    }
-    const int k0 = kt * BK;
-#pragma unroll
-    for (int pl = 0; pl < PL; ++pl)
-#pragma unroll
-      for (int j = 0; j < GB; ++j) {
-        const void* src = b_ok[j] ? static_cast<const void*>(b_ptr[j] + pl * wps + k0)
-                                  : static_cast<const void*>(zero + cbk * 16);
-        glds16(src, st + (CA + pl * CB + j * NT) * 16);
-      }
-    s_c0 += BK;
-    if (s_c0 >= d.Cin) {
-      s_c0 = 0;
-      if (++s_kw == d.KW) {
-        s_kw = 0;
-        ++s_kh;
-      }
-    }
-  };
-
-  const int wm = wave / WN;
-  const int wn = wave - wm * WN;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-
-  // M16: each 32×32 block of the wave as 2×2 blocks of v_mfma_f32_16x16x32_bf16 (lane l: A row l & 15,
-  // B column l & 15, k = 8(l >> 4) + j; C rows 4(l >> 4) + reg, column l & 15) on the same LDS images.
-  auto compute = [&](int buf) {
-    const uint4* st = smem + buf * STAGE;
-    if constexpr (M16) {
-      const int c16 = lane & 15, g = lane >> 4;
-      bf16x8 fb[2 * TN][PL];
-#pragma unroll
-      for (int j = 0; j < 2 * TN; ++j) {
-        const int brow = wn * TN * 32 + j * 16 + c16;
-#pragma unroll
-        for (int pl = 0; pl < PL; ++pl)
-          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + sw16(brow, g));
-      }
-#pragma unroll
-      for (int i = 0; i < 2 * TM; ++i) {
-        const int row = wm * TM * 32 + i * 16 + c16;
-        const int sz = (row >> 1) & 7;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
-        bf16x8 fa[PL];
-        split_frag_pk<PL>(x0, x1, fa);
-#pragma unroll
-        for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
-      }
-      return;
-    }
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      bf16x8 fb[TN][PL];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int brow = wn * TN * 32 + j * 32 + r;
-        const int bpos = BK == 64   ? brow * 8 + ((2 * s + h) ^ ((brow >> 1) & 7))
-                         : BK == 32 ? sw16(brow, 2 * s + h)
-                                    : brow * 2 + (h ^ ((brow >> 3) & 1));
-#pragma unroll
-        for (int pl = 0; pl < PL; ++pl)
-          fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 32 + i * 32 + r;
-        const int sz = BK == 64 ? row & 15 : BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
-        const int c0 = 4 * s + 2 * h;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
-        bf16x8 fa[PL];
-#if SP_ABLATE == 2  // no split: one cvt, planes aliased (same MFMA count)
-        {
-          bf16x8 hh;
-          hh[0] = (__bf16)x0.x; hh[1] = (__bf16)x0.y; hh[2] = (__bf16)x0.z; hh[3] = (__bf16)x0.w;
-          hh[4] = (__bf16)x1.x; hh[5] = (__bf16)x1.y; hh[6] = (__bf16)x1.z; hh[7] = (__bf16)x1.w;
-          for (int q = 0; q < PL; ++q) fa[q] = hh;
-        }
-#else
-        split_frag_pk<PL>(x0, x1, fa);
-#endif
-#if SP_ABLATE == 3  // no MFMA: keep the operands alive
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          for (int q = 0; q < PL; ++q) asm volatile("" ::"v"(fa[q]), "v"(fb[j][q]));
-#else
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_planes<PL>(fa, fb[j], acc[i][j]);
-#endif
-      }
-    }
-  };
-
-  // Prologue: stages 0 .. NS-2 in flight.
-#pragma unroll
-  for (int t = 0; t < NS - 1; ++t)
-    if (t < nk) issue(kt0 + t, t);
-  for (int kt = 0; kt < nk; ++kt) {
-    // retire stage kt: stages kt+1 .. min(kt+NS-2, nk-1) may stay in flight
-    const int ahead = (nk - 1 - kt) < (NS - 2) ? (nk - 1 - kt) : (NS - 2);
-    if (NS >= 6 && ahead >= 4) wait_vmcnt<(NS >= 6 ? 4 * GLDS : 0)>();
-    else if (NS >= 5 && ahead >= 3) wait_vmcnt<(NS >= 5 ? 3 * GLDS : 0)>();
-    else if (NS >= 4 && ahead >= 2) wait_vmcnt<(NS >= 4 ? 2 * GLDS : 0)>();
-    else if (NS >= 3 && ahead >= 1) wait_vmcnt<(NS >= 3 ? GLDS : 0)>();
-    else wait_vmcnt<0>();
-    raw_barrier();
-    if (kt == 0) GLDS_STAMP(1);
-#if SP_ABLATE == 1  // no DMA in the loop (compute on stale stages)
-    if (false)
-#else
-    if (kt + NS - 1 < nk)
-#endif
-      issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
-    compute(kt % NS);
+int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  switch (k) {
+    case 0: return glds_part<0>(a, planes, cfg, s);
+    case 1: return glds_part<1>(a, planes, cfg, s);
+    case 2: return glds_part<2>(a, planes, cfg, s);
+    case 3: return glds_part<3>(a, planes, cfg, s);
+    case 4: return glds_part<4>(a, planes, cfg, s);
+    default: return glds_part<5>(a, planes, cfg, s);
   }
 }
-
-template <int TM, int TN, bool M16>
-__device__ __forceinline__ void glds_zero(f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
-  if constexpr (M16) {
-#pragma unroll
-    for (int i = 0; i < 2 * TM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
-// Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
-// Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
-// index within that member.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
-__device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, int wg, f32x16 (&acc)[TM][TN],
-                                              f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  const int wm = wave / WN;
-  const int wn = wave - wm * WN;
-  const int tilesN = (p.d.Cout + C::BN - 1) / C::BN;
-  const int mt = wg / tilesN;
-  const int n0 = (wg - mt * tilesN) * C::BN;
-  const int64_t m0 = (int64_t)mt * C::BM;
-  float* smemf = reinterpret_cast<float*>(smem);
-  if constexpr (M16) {
-    // 16×16 blocks → the f32x16 of their 32×32 block: element q = 8·bi + 4·bj + reg
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc[i][j][q] = acc4[2 * i + (q >> 3)][2 * j + ((q >> 2) & 1)][q & 3];
-  }
-  epilogue_tile<TM, TN, C::NB, M16>(p, smemf + wave * (C::NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
-                                    n0 + wn * TN * 32, lane);
-}
-
-// OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained). Applied to the
-// 1×1 fast-path instantiations only (launch_glds): the general path's extra address registers spill.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1>
-__global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const ConvArgs p) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
-  __shared__ uint4 smem[C::SMEM];
-  GLDS_STAMP(0);
-  int wg = xcd_index(blockIdx.x, gridDim.x);
-  // batched launch (Winograd components): member bi owns tiles [bi·tiles_per_batch, (bi+1)·…)
-  const int bi = p.batch > 1 ? wg / p.tiles_per_batch : 0;
-  wg -= bi * p.tiles_per_batch;
-  const int nk_all = p.K / BK;
-  const int kt0 = (int)(((int64_t)nk_all * blockIdx.z) / p.splits);
-  const int kt1 = (int)(((int64_t)nk_all * (blockIdx.z + 1)) / p.splits);
-  f32x16 acc[TM][TN];
-  f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
-  glds_zero<TM, TN, M16>(acc, acc4);
-  glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V>(p, smem, wg, bi, kt0, kt1, acc, acc4);
-  GLDS_STAMP(2);
-  __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
-  ConvArgs q = p;
-  q.d.C += (int64_t)bi * p.bs_c;
-  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(q, smem, wg, acc, acc4);
-#if SP_GLDS_STAMP
-  __syncthreads();
-  GLDS_STAMP(3);
-  if (threadIdx.x == 0 && blockIdx.x < 16384) {
-    unsigned hw, xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    g_glds_stamps[blockIdx.x * 6 + 4] = hw;
-    g_glds_stamps[blockIdx.x * 6 + 5] = xcc;
-  }
-#endif
-}
-
-// The 1×1 fast path (V = 2) applies: KH = KW = 1, stride 1, no padding (A row m is A + m·lda), and
-// every byte offset of a batch member's A and weight plane fits 32 bits.
-inline bool t1_ok(const ConvArgs& a) {
-  const sp_conv_desc& d = a.d;
-  return d.KH == 1 && d.KW == 1 && d.stride == 1 && d.pad == 0 && d.Ho == d.H && d.Wo == d.W &&
-         a.M * d.lda * 4 < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
-}
-
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int OCC = 1>
-int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
-  if (a.d.Cin % BK || a.K % BK) {
-    set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
-    return -1;
-  }
-  constexpr int BM = 32 * TM * WM, BN = 32 * TN * WN;
-  const int64_t per = ((a.M + BM - 1) / BM) * ((a.d.Cout + BN - 1) / BN);
-  const int64_t tiles = per * a.batch;
-  if (tiles > 0x7fffffff || (a.batch > 1 && a.splits > 1)) {
-    set_error("sp_conv2d: %lld tiles exceed the grid (or split-K on a batched GEMM)", (long long)tiles);
-    return -1;
-  }
-  // a tile whose stages do not fit the 160 KB LDS for this operand mode is not instantiated
-  using C3 = GldsCfg<WM, WN, TM, TN, 3, NS, BK>;
-  using C1 = GldsCfg<WM, WN, TM, TN, 1, NS, BK>;
-  constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
-  if ((planes == 3 && !fit3) || (planes != 3 && !fit1)) {
-    set_error("sp_conv2d: tile stages exceed the LDS for %d operand plane(s)", planes);
-    return -1;
-  }
-  ConvArgs ab = a;
-  ab.tiles_per_batch = (int32_t)per;
-  dim3 grid((unsigned)tiles, 1, a.splits);
-  // the 1×1 fast path where it applies, else the general implicit GEMM
-  const bool t1 = t1_ok(a);
-  if constexpr (fit3) {
-    if (planes == 3 && t1)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC>), grid, dim3(64 * WM * WN), 0, s, ab);
-    else if (planes == 3)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
-  }
-  if constexpr (fit1) {
-    if (planes != 3 && t1)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC>), grid, dim3(64 * WM * WN), 0, s, ab);
-    else if (planes != 3)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, dim3(64 * WM * WN), 0, s, ab);
-  }
-  int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
-  if (rc || a.splits == 1) return rc;
-  return launch_splitk_reduce(a, s);
-}
-
 }  // namespace
+#else
+int launch_glds_part0(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part1(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part2(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part3(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part4(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part5(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+namespace {
+int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  switch (k) {
+    case 0: return launch_glds_part0(a, planes, cfg, s);
+    case 1: return launch_glds_part1(a, planes, cfg, s);
+    case 2: return launch_glds_part2(a, planes, cfg, s);
+    case 3: return launch_glds_part3(a, planes, cfg, s);
+    case 4: return launch_glds_part4(a, planes, cfg, s);
+    default: return launch_glds_part5(a, planes, cfg, s);
+  }
+}
+}  // namespace
+#endif
+static_assert(kGldsParts == 6, "one conv_glds_p<k>.hip per part");
 
 // The LDS-DMA configurations (see launch_mfma16); -2 when cfg is not one of them.
 int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
-  if (a.d.A2) return -2;
-  switch (cfg) {
-    case 11: return launch_glds<2, 2, 2, 2, 3>(a, planes, s);
-    case 12: return launch_glds<4, 2, 2, 2, 2>(a, planes, s);
-    case 13: return launch_glds<2, 2, 1, 2, 3>(a, planes, s);
-    case 14: return launch_glds<2, 2, 1, 1, 3>(a, planes, s);
-    case 15: return launch_glds<2, 4, 2, 2, 2>(a, planes, s);
-    case 16: return launch_glds<2, 2, 2, 1, 3>(a, planes, s);  // 128×64, 3 stages
-    case 17: return launch_glds<4, 1, 2, 4, 2>(a, planes, s);  // 256×128, 4 waves of 64×128
-    case 18: return launch_glds<2, 2, 2, 4, 2>(a, planes, s);  // 128×256, 4 waves of 64×128
-    case 19: return launch_glds<2, 1, 2, 4, 2>(a, planes, s);  // 128×128, 2 waves of 64×128, 2 stages
-    case 20: return launch_glds<2, 1, 2, 4, 3>(a, planes, s);  // 128×128, 2 waves of 64×128
-    case 33: return launch_glds<4, 2, 2, 4, 2>(a, planes, s);  // 256×256, 8 waves of 64×128
-    case 34: return launch_glds<2, 4, 4, 2, 2>(a, planes, s);  // 256×256, 8 waves of 128×64
-    case 35: return launch_glds<4, 1, 2, 4, 4, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 4 stages
-    case 36: return launch_glds<4, 1, 2, 4, 5, 16>(a, planes, s);  // 256×128 (4 waves of 64×128), k16 × 5 stages
-    case 37: return launch_glds<4, 2, 2, 4, 3, 16>(a, planes, s);  // 256×256, k16 stages × 3
-    case 38: return launch_glds<4, 2, 2, 4, 4, 16>(a, planes, s);  // 256×256, k16 stages × 4
-    case 41: return launch_glds<4, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 12 on 16x16x32 MFMAs
-    case 42: return launch_glds<4, 2, 2, 4, 2, 32, true>(a, planes, s);  // cfg 33 on 16x16x32 MFMAs
-    case 43: return launch_glds<2, 2, 2, 2, 3, 32, true>(a, planes, s);  // cfg 11 on 16x16x32 MFMAs
-    case 44: return launch_glds<4, 1, 2, 4, 2, 16>(a, planes, s);  // 256×128, 4 waves of 64×128, k16 × 2
-    case 45: return launch_glds<2, 2, 2, 2, 2>(a, planes, s);      // 128×128, k32 × 2 stages
-    // 128×128, k16 × 2 stages, registers for 4 waves per SIMD (four workgroups per CU): bit-identical,
-    // 1.02-1.09x over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
-    // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general
-    // path would spill: it keeps the unconstrained allocation)
-    case 46: return launch_glds<2, 2, 2, 2, 2, 16, false, 4>(a, planes, s);
-    case 47: return launch_glds<2, 2, 2, 2, 2, 32, true>(a, planes, s);  // cfg 45 on 16x16x32 MFMAs
-    case 48: return launch_glds<2, 2, 2, 4, 2, 16>(a, planes, s);  // 128×256, 4 waves of 64×128, k16 × 2
-    case 49: return launch_glds<4, 1, 2, 4, 2, 32, true>(a, planes, s);  // cfg 17 on 16x16x32 MFMAs
-    case 50: return launch_glds<4, 1, 2, 2, 3>(a, planes, s);      // 256×64, k32 × 3
-    case 51: return launch_glds<4, 1, 2, 2, 2>(a, planes, s);      // 256×64, k32 × 2
-    case 62: return launch_glds<4, 1, 1, 8, 2>(a, planes, s);      // 128×256, 4 waves of 32×256
-    case 63: return launch_glds<8, 1, 1, 4, 2>(a, planes, s);      // 256×128, 8 waves of 32×128
-    case 64: return launch_glds<4, 1, 1, 4, 3>(a, planes, s);      // 128×128, 4 waves of 32×128, 3 stages
-    case 65: return launch_glds<8, 1, 1, 4, 2, 32, true>(a, planes, s);  // cfg 63 on 16x16x32 MFMAs
-    default: return -2;
-  }
+  if (a.d.A2 || cfg < 11 || cfg > 65) return -2;
+  return glds_part_k(cfg % kGldsParts, a, planes, cfg, s);
 }
 
 }  // namespace sp

@@ -1,0 +1,11 @@
+// One part of the LDS-DMA tile configurations (conv_glds.h: ids with id % 6 == 1), compiled as its own
+// translation unit so the build runs the parts in parallel.
+#include "conv_glds.h"
+
+#if !SP_GLDS_STAMP
+namespace sp {
+int launch_glds_part1(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  return glds_part<1>(a, planes, cfg, s);
+}
+}  // namespace sp
+#endif
