@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 9
+#define SP_ABI_VERSION 10
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -96,6 +96,16 @@ typedef struct {
   const float* ln_gamma;
   const float* ln_beta;
   float ln_eps;
+  /* ABI v10: operands written as bf16 planes by their producer.
+   * A_bf16 (non-NULL) replaces A for sp_conv2d's LDS-DMA tiles: one bf16 plane (SP_PREC_BF16) or the
+   * hi / mid / lo planes of the split (SP_PREC_F32X3, a_plane_stride elements apart) — the GEMM then
+   * stages them as they are instead of rounding / splitting fp32 A per fragment; lda counts elements.
+   * wino_v_planes (sp_winograd_f43_*, SP_PREC_F32X3): the input transform writes V as its hi / mid /
+   * lo bf16 planes (the exact split the GEMM would compute) and the component GEMM stages them; the
+   * workspace then needs 36 * T * (1.5 * Cin + Cout) floats. Results are bit-identical either way. */
+  const uint16_t* A_bf16;
+  int64_t a_plane_stride;
+  int32_t wino_v_planes;
 } sp_conv_desc;
 
 /*

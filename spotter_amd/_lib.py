@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -42,6 +42,7 @@ class SpConvDesc(C.Structure):
         ("workspace", vp), ("workspace_elems", i64),
         ("precision", i32), ("Wt_bf16", vp), ("wt_plane_stride", i64),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
+        ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
     ]
 
 

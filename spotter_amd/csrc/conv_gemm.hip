@@ -293,7 +293,7 @@ extern "C" int sp_set_conv_config(int cfg) {
 extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   using namespace sp;
   SP_ARG_CHECK(d != nullptr, "sp_conv2d: null descriptor");
-  SP_ARG_CHECK(d->A && d->Wt && d->C, "sp_conv2d: null A/W/C");
+  SP_ARG_CHECK((d->A || d->A_bf16) && d->Wt && d->C, "sp_conv2d: null A/W/C");
   SP_ARG_CHECK(d->N > 0 && d->H > 0 && d->W > 0 && d->Cin > 0 && d->Cout > 0,
                "sp_conv2d: bad shape N=%d H=%d W=%d Cin=%d Cout=%d", d->N, d->H, d->W, d->Cin,
                d->Cout);
@@ -314,8 +314,16 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   SP_ARG_CHECK(planes < 3 || d->wt_plane_stride >= (int64_t)d->Cout * K,
                "sp_conv2d: wt_plane_stride %lld < Cout*K", (long long)d->wt_plane_stride);
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (d->A_bf16) {
+    SP_ARG_CHECK(planes > 0 && !d->A2 && !d->ln_gamma && d->Cin % BK == 0 && d->lda % 8 == 0 && al16(d->A_bf16) &&
+                     (planes == 1 || (d->a_plane_stride % 8 == 0 && d->a_plane_stride > 0)),
+                 "sp_conv2d: bf16 A planes need the bf16 / split operand mode, Cin %% 32 == 0, lda %% 8 == 0, "
+                 "16-byte aligned planes, no A2 / LayerNorm");
+  }
   ConvArgs a;
   a.d = *d;
+  a.A16 = d->A_bf16;
+  a.a_plane_stride = d->a_plane_stride;
   a.M = (int64_t)d->N * ho * wo;
   a.K = (int32_t)K;
   a.HoWo = ho * wo;
@@ -323,7 +331,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   // float4 / 8 x bf16 are 16-byte aligned.
   a.fast = (d->Cin % BK == 0) ? 1 : 0;
   if (a.fast) {
-    bool al = (d->lda % 4 == 0) && al16(d->A) && (!d->A2 || ((d->lda2 % 4 == 0) && al16(d->A2)));
+    bool al = d->A_bf16 || ((d->lda % 4 == 0) && al16(d->A) && (!d->A2 || ((d->lda2 % 4 == 0) && al16(d->A2))));
     al = al && (planes ? (al16(d->Wt_bf16) && (planes == 1 || d->wt_plane_stride % 8 == 0)) : al16(d->Wt));
     if (!al) a.fast = 0;
   }
@@ -350,7 +358,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     if (blocks64 < 64 && nk >= 8 && nk < 16) sp = nk / 4;
     else if (blocks64 < 256 && nk >= 16) sp = (int)((512 + blocks64 - 1) / blocks64), sp = sp < nk / 8 ? sp : nk / 8;
     else if (blocks64 < SP_SPLITK_BLOCKS && nk >= 64) sp = (int)((SP_SPLITK_BLOCKS + blocks64 - 1) / blocks64);
-    if (d->workspace && sp > 1) {
+    if (d->workspace && sp > 1 && !d->A_bf16) {  // split-K runs on the register-staged tiles (fp32 A)
       if (sp > 16) sp = 16;
       while (sp > 1 && (int64_t)sp * a.M * a.ldp > d->workspace_elems) --sp;
       if (sp > 1) a.splits = sp;

@@ -32,7 +32,7 @@ __device__ unsigned long long g_glds_stamps[16384 * 6];
 
 namespace {
 
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, int APL = 0>
 struct GldsCfg {
   // BK = 64 (4 k16 steps per barrier) is supported and was measured: 0.70-0.92x of the same wave tile at
   // k32 for both operand modes (profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per
@@ -42,13 +42,17 @@ struct GldsCfg {
   static constexpr int NT = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
-  static constexpr int RA = BK / 4;  // 16-byte chunks per fp32 A row (8 at BK = 32, 4 at BK = 16)
+  // APL: A planes in memory — 0: fp32 A, split per fragment; 1 / 3: bf16 planes (ConvArgs::A16)
+  static_assert(APL == 0 || APL == PL, "bf16 A planes match the operand mode");
+  static constexpr int RA = APL ? BK / 8 : BK / 4;  // 16-byte chunks per A row of one plane
   static constexpr int RB = BK / 8;  // 16-byte chunks per bf16 B row (4 / 2)
-  static constexpr int CA = BM * RA;  // 16-byte chunks of the fp32 A tile
+  static constexpr int CAP = BM * RA;  // 16-byte chunks of one A plane
+  static constexpr int CA = CAP * (APL ? APL : 1);  // ... of the whole A stage
   static constexpr int CB = BN * RB;  // 16-byte chunks of one bf16 B plane
+  static constexpr int GAP = CAP / NT;  // DMA pieces per thread per A plane
   static constexpr int GA = CA / NT;
   static constexpr int GB = CB / NT;
-  static_assert(GA * NT == CA && GB * NT == CB && GB >= 1, "DMA pieces must tile the workgroup");
+  static_assert(GAP * NT == CAP && GB * NT == CB && GB >= 1 && GAP >= 1, "DMA pieces must tile the workgroup");
   static constexpr int GLDS = GA + PL * GB;  // DMA instructions per thread per stage
   static constexpr int STAGE = CA + PL * CB;
   static constexpr int NB = (WM * WN * TM * 32 * TN * 32 / 4 <= NS * STAGE) ? TM : 1;
@@ -66,12 +70,14 @@ struct GldsCfg {
 // instead of a zero block. Both split A pair-wise (split_frag_pk). Bit-identical outputs, measured
 // 1.02-1.09× over the previous form (element-wise split, general addressing everywhere) on the C2
 // shapes (profiles/r3/ab_glds_v2.jsonl, tools/ab_glds.py).
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int APL = 0>
 __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
                                           f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
+  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;
   static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
   constexpr int NT = C::NT, RA = C::RA, RB = C::RB, CA = C::CA, CB = C::CB, GA = C::GA, GB = C::GB;
+  constexpr int CAP = C::CAP, GAP = C::GAP;
+  constexpr int ES = APL ? 2 : 4;  // bytes per A element
   constexpr int GLDS = C::GLDS, STAGE = C::STAGE, BM = C::BM, BN = C::BN;
 
   const sp_conv_desc& d = p.d;
@@ -85,19 +91,29 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   const int n0 = (wg - mt * tilesN) * BN;
   const int64_t m0 = (int64_t)mt * BM;
 
-  // A pieces: piece j of this thread covers tile row (j·NT + tid) / RA, LDS position tid % RA,
-  // global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of the
-  // swizzle period. swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way the
-  // 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
-  // BK = 64: an A row is 16 chunks = one whole 256-byte bank row, swizzle row & 15
-  const int ca = BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
+  // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
+  // (sw16), (row >> 3) & 1 at BK = 16.
+  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
+  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
+                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
+  // A pieces (per plane): piece j of this thread covers tile row (j·NT + tid) / RA, LDS position
+  // tid % RA, global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of
+  // the swizzle period. fp32 A: swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way
+  // the 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots;
+  // BK = 64: an A row is 16 chunks = one whole 256-byte bank row, swizzle row & 15. bf16 A planes: the
+  // B rows' swizzle.
+  const int ca = APL ? cbk
+               : BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
                : BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
-  const float* A = d.A + (int64_t)bi * p.bs_a;
+  const char* A = (APL ? reinterpret_cast<const char*>(p.A16) : reinterpret_cast<const char*>(d.A)) +
+                  (int64_t)bi * p.bs_a * ES;
+  constexpr int NAP = APL ? APL : 1;  // A planes staged
+  const int64_t aps = p.a_plane_stride * 2;  // bytes between bf16 A planes
   const uint16_t* Wt = d.Wt_bf16 + (int64_t)bi * p.bs_w;
-  int a_iy0[GA], a_ix0[GA];
-  const float* a_ptr[GA];
+  int a_iy0[GAP], a_ix0[GAP];
+  const char* a_ptr[GAP];
 #pragma unroll
-  for (int j = 0; j < GA; ++j) {
+  for (int j = 0; j < GAP; ++j) {
     const int64_t m = m0 + (j * NT + tid) / RA;
     const bool ok = m < p.M;
     const int64_t mm = ok ? m : 0;
@@ -107,13 +123,8 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     const int ox = rem - oy * d.Wo;
     a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
     a_ix0[j] = ox * d.stride - d.pad;
-    a_ptr[j] = A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda + ca * 4;
+    a_ptr[j] = A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda * ES + ca * 16;
   }
-  // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
-  // (sw16), (row >> 3) & 1 at BK = 16.
-  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
-  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
-                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
   const uint16_t* b_ptr[GB];
   bool b_ok[GB];
 #pragma unroll
@@ -124,12 +135,12 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   }
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
   // V == 2: byte offsets of this lane's A rows / B rows against the operand bases
-  uint32_t a_off[V == 2 ? GA : 1], b_off[V == 2 ? GB : 1];
+  uint32_t a_off[V == 2 ? GAP : 1], b_off[V == 2 ? GB : 1];
   if constexpr (V == 2) {
 #pragma unroll
-    for (int j = 0; j < GA; ++j) {
+    for (int j = 0; j < GAP; ++j) {
       const int64_t m = m0 + (j * NT + tid) / RA;
-      a_off[j] = (uint32_t)(((m < p.M ? m : p.M - 1) * d.lda + ca * 4) * 4);
+      a_off[j] = (uint32_t)((m < p.M ? m : p.M - 1) * d.lda * ES + ca * 16);
     }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
@@ -154,9 +165,12 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   auto issue = [&](int kt, int buf) {
     const uint32_t st = lds0 + (uint32_t)(buf * STAGE * 16) + wave_off;
     if constexpr (V == 2) {
-      const float* ab = A + (int64_t)kt * BK;
 #pragma unroll
-      for (int j = 0; j < GA; ++j) glds16s(a_off[j], ab, st + j * NT * 16);
+      for (int pl = 0; pl < NAP; ++pl) {
+        const char* ab = A + pl * aps + (int64_t)kt * BK * ES;
+#pragma unroll
+        for (int j = 0; j < GAP; ++j) glds16s(a_off[j], ab, st + (pl * CAP + j * NT) * 16);
+      }
 #pragma unroll
       for (int pl = 0; pl < PL; ++pl) {
         const uint16_t* bb = Wt + pl * wps + (int64_t)kt * BK;
@@ -165,12 +179,16 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
       }
       return;
     }
-    const int64_t off = ((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0;
+    const int64_t off = (((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0) * ES;
 #pragma unroll
-    for (int j = 0; j < GA; ++j) {
+    for (int j = 0; j < GAP; ++j) {
       const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
-      const void* src = ok ? static_cast<const void*>(a_ptr[j] + off) : static_cast<const void*>(zero + ca * 16);
-      glds16(src, st + j * NT * 16);
+#pragma unroll
+      for (int pl = 0; pl < NAP; ++pl) {
+        const void* src = ok ? static_cast<const void*>(a_ptr[j] + pl * aps + off)
+                             : static_cast<const void*>(zero + ca * 16);
+        glds16(src, st + (pl * CAP + j * NT) * 16);
+      }
     }
     const int k0 = kt * BK;
 #pragma unroll
@@ -213,11 +231,16 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int i = 0; i < 2 * TM; ++i) {
         const int row = wm * TM * 32 + i * 16 + c16;
-        const int sz = (row >> 1) & 7;
-        const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
-        const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
         bf16x8 fa[PL];
-        split_frag_pk<PL>(x0, x1, fa);
+        if constexpr (APL) {
+#pragma unroll
+          for (int pl = 0; pl < PL; ++pl) fa[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CAP + sw16(row, g));
+        } else {
+          const int sz = (row >> 1) & 7;
+          const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g) ^ sz));
+          const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((2 * g + 1) ^ sz));
+          split_frag_pk<PL>(x0, x1, fa);
+        }
 #pragma unroll
         for (int j = 0; j < 2 * TN; ++j) acc4[i][j] = mfma16x16_planes<PL>(fa, fb[j], acc4[i][j]);
       }
@@ -239,11 +262,18 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * TM * 32 + i * 32 + r;
+        bf16x8 fa[PL];
+        if constexpr (APL) {
+          const int apos = BK == 64   ? row * 8 + ((2 * s + h) ^ ((row >> 1) & 7))
+                           : BK == 32 ? sw16(row, 2 * s + h)
+                                      : row * 2 + (h ^ ((row >> 3) & 1));
+#pragma unroll
+          for (int pl = 0; pl < PL; ++pl) fa[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CAP + apos);
+        } else {
         const int sz = BK == 64 ? row & 15 : BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
         const int c0 = 4 * s + 2 * h;
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
-        bf16x8 fa[PL];
 #if SP_ABLATE == 2  // no split: one cvt, planes aliased (same MFMA count)
         {
           bf16x8 hh;
@@ -254,6 +284,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #else
         split_frag_pk<PL>(x0, x1, fa);
 #endif
+        }
 #if SP_ABLATE == 3  // no MFMA: keep the operands alive
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -337,9 +368,9 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
 
 // OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained). Applied to the
 // 1×1 fast-path instantiations only (launch_glds): the general path's extra address registers spill.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1, int APL = 0>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const ConvArgs p) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
+  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;
   __shared__ uint4 smem[C::SMEM];
   GLDS_STAMP(0);
   int wg = xcd_index(blockIdx.x, gridDim.x);
@@ -352,7 +383,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
   f32x16 acc[TM][TN];
   f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   glds_zero<TM, TN, M16>(acc, acc4);
-  glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V>(p, smem, wg, bi, kt0, kt1, acc, acc4);
+  glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V, APL>(p, smem, wg, bi, kt0, kt1, acc, acc4);
   GLDS_STAMP(2);
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   ConvArgs q = p;
@@ -376,10 +407,11 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
 inline bool t1_ok(const ConvArgs& a) {
   const sp_conv_desc& d = a.d;
   return d.KH == 1 && d.KW == 1 && d.stride == 1 && d.pad == 0 && d.Ho == d.H && d.Wo == d.W &&
-         a.M * d.lda * 4 < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
+         a.M * d.lda * (a.A16 ? 2 : 4) < (int64_t(1) << 32) && (int64_t)d.Cout * a.K * 2 < (int64_t(1) << 32);
 }
 
-template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int OCC = 1>
+// AB: the bf16-A-plane variants (ConvArgs::A16) are compiled for this tile.
+template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int OCC = 1, bool AB = false>
 int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   if (a.d.Cin % BK || a.K % BK) {
     set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
@@ -395,9 +427,14 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   // a tile whose stages do not fit the 160 KB LDS for this operand mode is not instantiated
   using C3 = GldsCfg<WM, WN, TM, TN, 3, NS, BK>;
   using C1 = GldsCfg<WM, WN, TM, TN, 1, NS, BK>;
+  using C3a = GldsCfg<WM, WN, TM, TN, 3, NS, BK, 3>;
+  using C1a = GldsCfg<WM, WN, TM, TN, 1, NS, BK, 1>;
   constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
-  if ((planes == 3 && !fit3) || (planes != 3 && !fit1)) {
-    set_error("sp_conv2d: tile stages exceed the LDS for %d operand plane(s)", planes);
+  constexpr bool fit3a = AB && C3a::SMEM * 16 <= 163840, fit1a = AB && C1a::SMEM * 16 <= 163840;
+  const bool a16 = a.A16 != nullptr;
+  if ((planes == 3 && !(a16 ? fit3a : fit3)) || (planes != 3 && !(a16 ? fit1a : fit1))) {
+    set_error("sp_conv2d: tile configuration not built for %d operand plane(s)%s (LDS or bf16-A variant)", planes,
+              a16 ? " with bf16 A planes" : "");
     return -1;
   }
   ConvArgs ab = a;
@@ -407,16 +444,28 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   const bool t1 = t1_ok(a);
   const dim3 blk(64 * WM * WN);
   if constexpr (fit3) {
-    if (planes == 3 && t1)
+    if (planes == 3 && !a16 && t1)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC>), grid, blk, 0, s, ab);
-    else if (planes == 3)
+    else if (planes == 3 && !a16)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, blk, 0, s, ab);
   }
   if constexpr (fit1) {
-    if (planes != 3 && t1)
+    if (planes != 3 && !a16 && t1)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC>), grid, blk, 0, s, ab);
-    else if (planes != 3)
+    else if (planes != 3 && !a16)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, blk, 0, s, ab);
+  }
+  if constexpr (fit3a) {
+    if (planes == 3 && a16 && t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 3>), grid, blk, 0, s, ab);
+    else if (planes == 3 && a16)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1, 1, 3>), grid, blk, 0, s, ab);
+  }
+  if constexpr (fit1a) {
+    if (planes != 3 && a16 && t1)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC, 1>), grid, blk, 0, s, ab);
+    else if (planes != 3 && a16)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1, 1, 1>), grid, blk, 0, s, ab);
   }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
   if (rc || a.splits == 1) return rc;
@@ -424,41 +473,41 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
 }
 
 
-// The LDS-DMA tile configurations: (id, WM, WN, TM, TN, NS, BK, M16, OCC). Tile BM × BN = 32·TM·WM ×
+// The LDS-DMA tile configurations: (id, WM, WN, TM, TN, NS, BK, M16, OCC, AB). Tile BM × BN = 32·TM·WM ×
 // 32·TN·WN, WM × WN waves, NS stages of BK-deep k, M16: v_mfma_f32_16x16x32_bf16 blocks, OCC: the
-// register budget of the 1×1 fast path (waves per SIMD).
+// register budget of the 1×1 fast path (waves per SIMD), AB: bf16-A-plane variants compiled.
 #define SP_GLDS_CONFIGS(X)              \
-  X(11, 2, 2, 2, 2, 3, 32, false, 1)    \
-  X(12, 4, 2, 2, 2, 2, 32, false, 1)    \
-  X(13, 2, 2, 1, 2, 3, 32, false, 1)    \
-  X(14, 2, 2, 1, 1, 3, 32, false, 1)    \
-  X(15, 2, 4, 2, 2, 2, 32, false, 1)    \
-  X(16, 2, 2, 2, 1, 3, 32, false, 1)    /* 128×64, 3 stages */ \
-  X(17, 4, 1, 2, 4, 2, 32, false, 1)    /* 256×128, 4 waves of 64×128 */ \
-  X(18, 2, 2, 2, 4, 2, 32, false, 1)    /* 128×256, 4 waves of 64×128 */ \
-  X(19, 2, 1, 2, 4, 2, 32, false, 1)    /* 128×128, 2 waves of 64×128, 2 stages */ \
-  X(20, 2, 1, 2, 4, 3, 32, false, 1)    /* 128×128, 2 waves of 64×128 */ \
-  X(33, 4, 2, 2, 4, 2, 32, false, 1)    /* 256×256, 8 waves of 64×128 */ \
-  X(34, 2, 4, 4, 2, 2, 32, false, 1)    /* 256×256, 8 waves of 128×64 */ \
-  X(35, 4, 1, 2, 4, 4, 16, false, 1)    /* 256×128, k16 × 4 stages */ \
-  X(36, 4, 1, 2, 4, 5, 16, false, 1)    /* 256×128, k16 × 5 stages */ \
-  X(37, 4, 2, 2, 4, 3, 16, false, 1)    /* 256×256, k16 × 3 */ \
-  X(38, 4, 2, 2, 4, 4, 16, false, 1)    /* 256×256, k16 × 4 */ \
-  X(41, 4, 2, 2, 2, 2, 32, true, 1)     /* cfg 12 on 16x16x32 MFMAs */ \
-  X(42, 4, 2, 2, 4, 2, 32, true, 1)     /* cfg 33 on 16x16x32 MFMAs */ \
-  X(43, 2, 2, 2, 2, 3, 32, true, 1)     /* cfg 11 on 16x16x32 MFMAs */ \
-  X(44, 4, 1, 2, 4, 2, 16, false, 1)    /* 256×128, 4 waves of 64×128, k16 × 2 */ \
-  X(45, 2, 2, 2, 2, 2, 32, false, 1)    /* 128×128, k32 × 2 */ \
-  X(46, 2, 2, 2, 2, 2, 16, false, 4)    /* 128×128, k16 × 2, four workgroups per CU (see below) */ \
-  X(47, 2, 2, 2, 2, 2, 32, true, 1)     /* cfg 45 on 16x16x32 MFMAs */ \
-  X(48, 2, 2, 2, 4, 2, 16, false, 1)    /* 128×256, 4 waves of 64×128, k16 × 2 */ \
-  X(49, 4, 1, 2, 4, 2, 32, true, 1)     /* cfg 17 on 16x16x32 MFMAs */ \
-  X(50, 4, 1, 2, 2, 3, 32, false, 1)    /* 256×64, k32 × 3 */ \
-  X(51, 4, 1, 2, 2, 2, 32, false, 1)    /* 256×64, k32 × 2 */ \
-  X(62, 4, 1, 1, 8, 2, 32, false, 1)    /* 128×256, 4 waves of 32×256 */ \
-  X(63, 8, 1, 1, 4, 2, 32, false, 1)    /* 256×128, 8 waves of 32×128 */ \
-  X(64, 4, 1, 1, 4, 3, 32, false, 1)    /* 128×128, 4 waves of 32×128, 3 stages */ \
-  X(65, 8, 1, 1, 4, 2, 32, true, 1)     /* cfg 63 on 16x16x32 MFMAs */
+  X(11, 2, 2, 2, 2, 3, 32, false, 1, false)    \
+  X(12, 4, 2, 2, 2, 2, 32, false, 1, true)    \
+  X(13, 2, 2, 1, 2, 3, 32, false, 1, true)    \
+  X(14, 2, 2, 1, 1, 3, 32, false, 1, true)    \
+  X(15, 2, 4, 2, 2, 2, 32, false, 1, false)    \
+  X(16, 2, 2, 2, 1, 3, 32, false, 1, true)    /* 128×64, 3 stages */ \
+  X(17, 4, 1, 2, 4, 2, 32, false, 1, false)    /* 256×128, 4 waves of 64×128 */ \
+  X(18, 2, 2, 2, 4, 2, 32, false, 1, false)    /* 128×256, 4 waves of 64×128 */ \
+  X(19, 2, 1, 2, 4, 2, 32, false, 1, false)    /* 128×128, 2 waves of 64×128, 2 stages */ \
+  X(20, 2, 1, 2, 4, 3, 32, false, 1, false)    /* 128×128, 2 waves of 64×128 */ \
+  X(33, 4, 2, 2, 4, 2, 32, false, 1, true)    /* 256×256, 8 waves of 64×128 */ \
+  X(34, 2, 4, 4, 2, 2, 32, false, 1, false)    /* 256×256, 8 waves of 128×64 */ \
+  X(35, 4, 1, 2, 4, 4, 16, false, 1, false)    /* 256×128, k16 × 4 stages */ \
+  X(36, 4, 1, 2, 4, 5, 16, false, 1, false)    /* 256×128, k16 × 5 stages */ \
+  X(37, 4, 2, 2, 4, 3, 16, false, 1, false)    /* 256×256, k16 × 3 */ \
+  X(38, 4, 2, 2, 4, 4, 16, false, 1, false)    /* 256×256, k16 × 4 */ \
+  X(41, 4, 2, 2, 2, 2, 32, true, 1, true)     /* cfg 12 on 16x16x32 MFMAs */ \
+  X(42, 4, 2, 2, 4, 2, 32, true, 1, true)     /* cfg 33 on 16x16x32 MFMAs */ \
+  X(43, 2, 2, 2, 2, 3, 32, true, 1, false)     /* cfg 11 on 16x16x32 MFMAs */ \
+  X(44, 4, 1, 2, 4, 2, 16, false, 1, true)    /* 256×128, 4 waves of 64×128, k16 × 2 */ \
+  X(45, 2, 2, 2, 2, 2, 32, false, 1, true)    /* 128×128, k32 × 2 */ \
+  X(46, 2, 2, 2, 2, 2, 16, false, 4, true)    /* 128×128, k16 × 2, four workgroups per CU (see below) */ \
+  X(47, 2, 2, 2, 2, 2, 32, true, 1, true)     /* cfg 45 on 16x16x32 MFMAs */ \
+  X(48, 2, 2, 2, 4, 2, 16, false, 1, false)    /* 128×256, 4 waves of 64×128, k16 × 2 */ \
+  X(49, 4, 1, 2, 4, 2, 32, true, 1, false)     /* cfg 17 on 16x16x32 MFMAs */ \
+  X(50, 4, 1, 2, 2, 3, 32, false, 1, false)    /* 256×64, k32 × 3 */ \
+  X(51, 4, 1, 2, 2, 2, 32, false, 1, true)    /* 256×64, k32 × 2 */ \
+  X(62, 4, 1, 1, 8, 2, 32, false, 1, false)    /* 128×256, 4 waves of 32×256 */ \
+  X(63, 8, 1, 1, 4, 2, 32, false, 1, true)    /* 256×128, 8 waves of 32×128 */ \
+  X(64, 4, 1, 1, 4, 3, 32, false, 1, true)    /* 128×128, 4 waves of 32×128, 3 stages */ \
+  X(65, 8, 1, 1, 4, 2, 32, true, 1, false)     /* cfg 63 on 16x16x32 MFMAs */
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path
@@ -471,10 +520,10 @@ constexpr int kGldsParts = 6;
 template <int PART>
 int glds_part(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   switch (cfg) {
-#define SP_GLDS_CASE(id, WM, WN, TM, TN, NS, BK, M16, OCC)                            \
+#define SP_GLDS_CASE(id, WM, WN, TM, TN, NS, BK, M16, OCC, AB)                          \
   case id:                                                                            \
     if constexpr ((id) % kGldsParts == PART)                                          \
-      return launch_glds<WM, WN, TM, TN, NS, BK, M16, OCC>(a, planes, s);        \
+      return launch_glds<WM, WN, TM, TN, NS, BK, M16, OCC, AB>(a, planes, s);        \
     else                                                                              \
       return -2;
     SP_GLDS_CONFIGS(SP_GLDS_CASE)

@@ -1356,6 +1356,26 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
 // cfg (LDS-DMA kernel, no A2): 11 = 128×128 3 stages, 12 = 256×128 2 stages, 13 = 64×128 3 stages,
 // 14 = 64×64 3 stages, 15 = 128×256 2 stages, 16 = 128×64 3 stages; < 0 = by shape.
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  if (a.A16) {  // bf16 A planes: the LDS-DMA tiles only (the forced / table tile, else the by-shape rule's)
+    if (cfg >= 11) {
+      const int rc = launch_glds_cfg(a, planes, cfg, s);
+      if (rc != -2) return rc;
+    }
+    int c = -1;
+    const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };
+    if (a.d.Cout <= 64) c = tiles(128, 64) >= 192 ? 16 : 14;
+    else if (a.d.Cout % 256 == 0 && a.K >= 512 && tiles(256, 256) >= 192) c = 33;
+    else if (a.d.Cout % 128 == 0 && tiles(128, 128) >= 192) c = planes == 3 ? 46 : 45;
+    else if (tiles(256, 128) >= 192) c = 12;
+    else if (tiles(64, 128) >= 192) c = 13;
+    else c = 14;
+    const int rc = launch_glds_cfg(a, planes, c, s);
+    if (rc == -2) {
+      set_error("sp_conv2d: no LDS-DMA tile for bf16 A planes");
+      return -1;
+    }
+    return rc;
+  }
   if (!a.fast) {  // generic gather: one small-tile instance per operand mode
     const int64_t tiles = ((a.M + 63) / 64) * ((a.d.Cout + 63) / 64);
     dim3 grid((unsigned)tiles, 1, a.splits);

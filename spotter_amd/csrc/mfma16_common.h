@@ -77,7 +77,7 @@ __device__ __forceinline__ f32x4 mfma16x16_planes(const bf16x8* a, const bf16x8*
 // position q of A row r holds global chunk q ^ ((r >> 1) & 7) (conflict-free b128 fragment reads,
 // the fp32 kernel's swizzle), position q of a B row holds chunk q ^ ((r >> 2) & 3) (sw16).
 // Padding taps, rows past M and columns past Cout read a 128-byte zero block instead.
-__device__ float4 g_zero_chunk[8];
+__device__ float4 g_zero_chunk[16];  // 256 B: the widest staged row chunk offset (fp32 A at BK = 64) stays inside
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));

@@ -150,7 +150,7 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4):
+                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -179,6 +179,11 @@ class Engine:
         if wino_m not in (2, 4):
             raise ValueError("wino_m must be 2 (F(2x2,3x3)) or 4 (F(4x4,3x3))")
         self.wino_m = wino_m
+        # F(4x4) on the split mode with the input transform writing V as the GEMM's hi / mid / lo bf16 planes
+        # (sp_conv_desc.wino_v_planes) instead of fp32 V split again per GEMM fragment: bit-identical
+        # (tests/test_gpu_kernels.py) but 0.70-0.87x on the C2 shapes (profiles/r3/x3/ab_wino_v_planes.jsonl:
+        # V grows 1.5x and these short-K GEMMs move as many bytes as they do MFMA work), so off by default
+        self.wino_v_planes = wino_v_planes
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
@@ -434,9 +439,10 @@ class Engine:
         if cw.wino is not None and stride == 1 and not kw and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
-            work = self._buf("wino_work", (wm + 2) ** 2 * tiles * (cw.cin + cw.cout))
+            vpl = self.wino_v_planes and wm == 4 and cw.wino.shape[0] == 3
+            work = self._buf("wino_work", ops.wino_work_elems(wm, tiles, cw.cin, cw.cout, vpl))
             return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, 3, 1, 1, out, scale=cw.scale, shift=cw.shift,
-                              act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm))
+                              act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm, vpl))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
                           workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)

@@ -306,6 +306,87 @@ def test_winograd_epilogue_views_and_bf16(dev, wm):
     assert np.abs(d16).max() <= 0.05 * np.abs(plain.cpu().numpy()).max(), np.abs(d16).max()
 
 
+@pytest.mark.parametrize("case", WINO_CASES + [(2, 13, 40, 128, 160, "relu")])
+@pytest.mark.parametrize("cfg", [None, "46", "47", "44", "14", "33"])
+def test_winograd_v_planes_bit_identical(dev, case, cfg):
+    """F(4×4) with the input transform writing V as the split GEMM's hi / mid / lo bf16 planes
+    (sp_conv_desc.wino_v_planes, ABI v10) gives exactly the fp32-V result: the transform rounds the same V
+    values the GEMM would split per fragment, and the GEMM stages the planes as they are. With BN, res1,
+    an input channel slice (lda > Cin) and an output slice (ldc > Cout)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    n, h, w, cin, cout, act = case
+    rng = np.random.default_rng(seed(case, 17))
+    m = n * h * w
+    big = rng.standard_normal((m, cin + 32)).astype(np.float32)
+    wt = (rng.standard_normal((cout, 3, 3, cin)) / np.sqrt(9 * cin)).astype(np.float32)
+    kw = dict(scale=T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev),
+              shift=T(rng.standard_normal(cout).astype(np.float32), dev), act=act,
+              res1=V(T(rng.standard_normal(m * cout).astype(np.float32), dev), 0, cout))
+    xd = V(T(big.reshape(-1), dev), 32, cin + 32)
+    wk = T(wt.reshape(cout, -1), dev)
+    planes = T(ops.split_bf16x3_host(ops.winograd_weights_host(wt, 4)), dev)
+    tiles = n * ((h + 3) // 4) * ((w + 3) // 4)
+    outs = []
+    for vpl in (False, True):
+        work = torch.full((ops.wino_work_elems(4, tiles, cin, cout, vpl),), float("nan"), device=dev)
+        out = torch.full((m * (cout + 8),), -7.0, device=dev)
+        ops.force_conv_config(cfg)
+        try:
+            ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(out, 8, cout + 8), wino=(planes, work, 4, vpl), **kw)
+        except RuntimeError as e:  # a forced tile that cannot take this shape / operand form
+            ops.force_conv_config(None)
+            pytest.skip(str(e))
+        ops.force_conv_config(None)
+        outs.append(out.cpu().numpy())
+    assert not np.isnan(outs[1]).any()
+    assert np.array_equal(outs[0], outs[1]), np.abs(outs[0] - outs[1]).max()
+
+
+def test_conv2d_bf16_a_planes_bit_identical(dev):
+    """sp_conv2d with A given as bf16 planes (sp_conv_desc.A_bf16, ABI v10) equals the fp32-A launch when
+    the planes hold the exact split (x3) / rounding (bf16) of that fp32 A: 1×1 and 3×3 stride-2 convs,
+    ragged M / Cout, residual epilogue, every LDS-DMA tile that builds the bf16-A form."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(23)
+    for (n, h, w, cin, cout, k, stride) in [(2, 9, 13, 64, 96, 1, 1), (1, 17, 15, 32, 72, 3, 2),
+                                             (3, 8, 8, 128, 256, 3, 1)]:
+        x = rng.standard_normal((n * h * w, cin)).astype(np.float32)
+        wt = (rng.standard_normal((cout, k * k * cin)) / np.sqrt(k * k * cin)).astype(np.float32)
+        ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (w + 2 * (k // 2) - k) // stride + 1
+        res = rng.standard_normal((n * ho * wo, cout)).astype(np.float32)
+        wk = T(wt, dev)
+        xs = ops.split_bf16x3_host(x)  # [3, rows·cin] hi / mid / lo
+        for mode in ("x3", "bf16"):
+            pl = xs if mode == "x3" else xs[:1]
+            a16 = T(np.ascontiguousarray(pl).reshape(-1).view(np.int16), dev)
+            wkw = dict(wt_planes=ops.split_bf16x3(wk)) if mode == "x3" else dict(
+                wt16=T(ops.bf16_bits(wt).view(np.int16), dev))
+            for cfg in (None, "14", "46", "45", "12", "33", "47", "63", "16"):
+                outs = []
+                for use16 in (False, True):
+                    out = torch.full((n * ho * wo * cout,), float("nan"), device=dev)
+                    xin = T(x.reshape(-1), dev) if mode == "x3" else T(ops._bf16_float(xs[0]).reshape(-1), dev)
+                    ops.force_conv_config(cfg)
+                    try:
+                        ops.conv2d(V(xin, 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2, V(out, 0, cout),
+                                   res1=V(T(res.reshape(-1), dev), 0, cout), act="relu",
+                                   a_bf16=(a16, x.size) if use16 else None, **wkw)
+                    except RuntimeError as e:
+                        ops.force_conv_config(None)
+                        outs.append(str(e))
+                        continue
+                    ops.force_conv_config(None)
+                    outs.append(out.cpu().numpy())
+                if any(isinstance(o, str) for o in outs):
+                    assert cfg is not None, outs  # only a forced tile may lack the form
+                    continue
+                assert np.array_equal(outs[0], outs[1]), (mode, cfg, k, np.abs(outs[0] - outs[1]).max())
+
+
 def test_conv2d_f32x3_epilogue_and_views(dev):
     """The split path shares the fused epilogue: BN, residuals, act, A2, row mask, grouped rows."""
     from spotter_amd import ops

@@ -40,6 +40,14 @@ EDGES = [(1, 1, 1000, 256, 192, True, "relu"), (3, 7, 9, 128, 320, False, None),
 
 
 PLANES = 3  # 3 = the fp32-accurate split (x3), 1 = the bf16 operand mode (--planes 1)
+VPL = False  # Winograd V as split bf16 planes (configuration suffix "v")
+
+
+def force(c):
+    """Select configuration c ("46", "46v": the same tile with Winograd V planes, "-": none)."""
+    global VPL
+    VPL = c.endswith("v")
+    ops.force_conv_config(c.rstrip("v") or None)
 
 
 def make(dev, shape, seed=0):
@@ -58,7 +66,8 @@ def make(dev, shape, seed=0):
         u = ops.winograd_weights_host(wt.view(cout, 3, 3, cin).cpu().numpy(), 4)
         planes = (torch.from_numpy(ops.split_bf16x3_host(u)).to(dev) if PLANES == 3 else
                   torch.from_numpy(ops.bf16_bits(u).reshape(1, -1).view("int16")).to(dev))
-        work = torch.empty(36 * (n * ((h + 3) // 4) * ((w + 3) // 4)) * (cin + cout), device=dev)
+        t = n * ((h + 3) // 4) * ((w + 3) // 4)
+        work = torch.empty(ops.wino_work_elems(4, t, cin, cout, True), device=dev)
         kw["wino"] = (planes, work, 4)
     elif PLANES == 3:
         kw["wt_planes"] = ops.split_bf16x3(wt)
@@ -67,8 +76,11 @@ def make(dev, shape, seed=0):
     act = None if wino else shape[6]
 
     def run():
+        kk = dict(kw)
+        if wino:  # a configuration "<cfg>v" runs the Winograd conv with V as bf16 split planes
+            kk["wino"] = kw["wino"] + (VPL,)
         ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, 1, k // 2, view(out, cout), scale=sc, shift=sh,
-                   act=act, res1=view(res, cout) if res is not None else None, **kw)
+                   act=act, res1=view(res, cout) if res is not None else None, **kk)
 
     flops = 2.0 * n * h * w * cout * cin * (9 if wino else 1)  # direct-equivalent for Winograd
     if wino:
@@ -113,7 +125,7 @@ def main():
         for c0, c1 in pairs:
             res = []
             for c in (c0, c1):
-                ops.force_conv_config(c)
+                force(c)
                 out.fill_(float("nan"))
                 try:
                     run()
@@ -122,7 +134,7 @@ def main():
                     continue
                 torch.cuda.synchronize()
                 res.append(out.clone())
-            ops.force_conv_config("-")
+            force("-")
             if any(isinstance(r, str) for r in res):
                 emit({"check": list(shape), "pair": [c0, c1], "skipped": [r for r in res if isinstance(r, str)]})
                 continue
@@ -140,14 +152,14 @@ def main():
             ok = True
             for _ in range(a.rounds):
                 for c in (c0, c1):
-                    ops.force_conv_config(c)
+                    force(c)
                     try:
                         run()
                         torch.cuda.synchronize()
                         t[c].append(timed(run, a.reps))
                     except RuntimeError:
                         ok = False
-            ops.force_conv_config("-")
+            force("-")
             if not ok or not t[c0] or not t[c1]:
                 continue
             m0, m1 = statistics.median(t[c0]), statistics.median(t[c1])
