@@ -65,6 +65,8 @@ def parse():
                     help="stride-1 3x3 convs as Winograd (default: the Engine's product default)")
     ap.add_argument("--wino-m", type=int, default=None, choices=[2, 4],
                     help="Winograd output tile: F(2x2,3x3) or F(4x4,3x3) (default: the Engine's)")
+    ap.add_argument("--fp32-maps", action="store_true",
+                    help="bf16 modes: keep the backbone maps in fp32 (A/B of the bf16 activation storage)")
     ap.add_argument("--microbatches", type=int, default=None,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
@@ -403,6 +405,8 @@ def make_step(args, rank, local):
     ekw = {} if args.winograd is None else {"winograd": False if args.winograd == "off" else args.winograd}
     if args.wino_m is not None:
         ekw["wino_m"] = args.wino_m
+    if args.fp32_maps:
+        ekw["bf16_store"] = False
     eng = Engine(cfg, weights, dev, precision=args.precision, **ekw)
     if args.microbatches is not None:
         eng.microbatches = args.microbatches

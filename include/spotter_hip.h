@@ -106,6 +106,11 @@ typedef struct {
   const uint16_t* A_bf16;
   int64_t a_plane_stride;
   int32_t wino_v_planes;
+  /* ABI v10: bf16 activations (the bf16 variant keeps the backbone's maps in bf16). C_bf16 (non-NULL)
+   * replaces C: the epilogue result is stored as bf16 (RNE) rows, ldc / out_group_stride in elements.
+   * res1_bf16 (non-NULL) replaces res1 (bf16 rows, ldr1 in elements). Not with LayerNorm. */
+  uint16_t* C_bf16;
+  const uint16_t* res1_bf16;
 } sp_conv_desc;
 
 /*
@@ -185,11 +190,18 @@ int sp_nchw_to_nhwc(const float* x, float* y, int n, int c, int h, int w, void* 
  * act 0 (none) or 1 (relu). (ABI v6) */
 int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, const float* shift, float* y,
                            int n, int h, int w, int cout, int act, void* stream);
+/* The same with bf16 output rows (ABI v10: the bf16 variant; fp32 arithmetic, RNE at the store). */
+int sp_stem_conv3x3s2_nchw_bf16(const float* x, const float* wt, const float* scale, const float* shift, uint16_t* y,
+                                int n, int h, int w, int cout, int act, void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
  * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
 int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);
+/* The same on bf16 rows (ABI v10: the bf16 variant's backbone maps); c % 8 == 0, ldy % 8 == 0. */
+int sp_maxpool3x3s2_bf16(const uint16_t* x, uint16_t* y, int64_t ldy, int n, int h, int w, int c, void* stream);
 /* nn.AvgPool2d(2, 2, 0, ceil_mode=True) on NHWC (RN:150, RN:202); y rows ldy floats apart as above. */
 int sp_avgpool2x2_ceil(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);
+/* The same on bf16 rows (ABI v10; fp32 sum and divide, RNE to bf16); c % 8 == 0, ldy % 8 == 0. */
+int sp_avgpool2x2_ceil_bf16(const uint16_t* x, uint16_t* y, int64_t ldy, int n, int h, int w, int c, void* stream);
 /* F.interpolate(scale_factor=2, mode="nearest") into a channel slice (M2:1192). */
 int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, int n, int h,
                           int w, int c, void* stream);

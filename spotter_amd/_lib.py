@@ -43,6 +43,7 @@ class SpConvDesc(C.Structure):
         ("precision", i32), ("Wt_bf16", vp), ("wt_plane_stride", i64),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
+        ("C_bf16", vp), ("res1_bf16", vp),
     ]
 
 
@@ -78,6 +79,9 @@ _SIGS = {
     "sp_stem_conv3x3s2_nchw": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_maxpool3x3s2": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
     "sp_avgpool2x2_ceil": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
+    "sp_maxpool3x3s2_bf16": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
+    "sp_avgpool2x2_ceil_bf16": (i32, [vp, vp, i64, i32, i32, i32, i32, vp]),
+    "sp_stem_conv3x3s2_nchw_bf16": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_upsample2x_nearest": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_layernorm": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),
     "sp_attention": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),

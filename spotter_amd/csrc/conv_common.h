@@ -38,11 +38,43 @@ struct ConvArgs {
   int64_t a_plane_stride = 0;
 };
 
-// Output row pointer: plain row-major (out_rows_per_group == 0) or grouped rows.
-__device__ __forceinline__ float* out_row(const sp_conv_desc& d, int64_t m) {
-  if (d.out_rows_per_group <= 0) return d.C + m * d.ldc;
+// Output row offset (elements): plain row-major (out_rows_per_group == 0) or grouped rows.
+__device__ __forceinline__ int64_t out_off(const sp_conv_desc& d, int64_t m) {
+  if (d.out_rows_per_group <= 0) return m * d.ldc;
   const int64_t g = m / d.out_rows_per_group;
-  return d.C + g * d.out_group_stride + (m - g * d.out_rows_per_group) * d.ldc;
+  return g * d.out_group_stride + (m - g * d.out_rows_per_group) * d.ldc;
+}
+__device__ __forceinline__ float* out_row(const sp_conv_desc& d, int64_t m) { return d.C + out_off(d, m); }
+
+// bf16 activations in HBM (ABI v10: sp_conv_desc.C_bf16 / res1_bf16). bf16 → fp32 is exact; fp32 → bf16
+// rounds to nearest even (v_cvt_pk_bf16_f32).
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+// The res1 row segment n..n+3 of row m (fp32 or bf16 residual rows), zero without a residual.
+__device__ __forceinline__ float4 load_res1(const sp_conv_desc& d, int64_t m, int n) {
+  if (d.res1_bf16) {
+    const uint2 u = *reinterpret_cast<const uint2*>(d.res1_bf16 + m * d.ldr1 + n);
+    return make_float4(bf16_lo(u.x), bf16_hi(u.x), bf16_lo(u.y), bf16_hi(u.y));
+  }
+  if (d.res1) return *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n);
+  return make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ bool has_res1(const sp_conv_desc& d) { return d.res1 || d.res1_bf16; }
+
+// Store the finished float4 of row m, channels n..n+3 (fp32 rows or bf16 rows).
+__device__ __forceinline__ void store_out4(const sp_conv_desc& d, int64_t m, int n, float4 v) {
+  if (d.C_bf16) {
+    *reinterpret_cast<uint2*>(d.C_bf16 + out_off(d, m) + n) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  } else {
+    *reinterpret_cast<float4*>(out_row(d, m) + n) = v;
+  }
 }
 
 // The fused epilogue on four consecutive output channels n..n+3 of row m (p.vec_epi, n+3 < Cout),
@@ -57,7 +89,7 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
   const float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y);
   v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
-  if (d.res1) {
+  if (has_res1(d)) {
     v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
   }
   v.x = act_apply(v.x, d.act); v.y = act_apply(v.y, d.act);
@@ -66,18 +98,16 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
     const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
     v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
   }
-  *reinterpret_cast<float4*>(out_row(d, m) + n) = v;
+  store_out4(d, m, n, v);
 }
 
 // The fused epilogue on four consecutive output channels n..n+3 of row m.
 __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int n, float4 v) {
   const sp_conv_desc& d = p.d;
   if (p.vec_epi && n + 3 < d.Cout) {
-    const float4 r1 = d.res1 ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-    epilogue_vec(p, m, n, v, r1);
+    epilogue_vec(p, m, n, v, load_res1(d, m, n));
   } else {
-    float* crow = out_row(d, m);
+    const int64_t ro = out_off(d, m);
     float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -87,9 +117,11 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int
       if (d.row_scale) x *= d.row_scale[m % d.row_period];
       x = fmaf(x, d.scale ? d.scale[nn] : 1.0f, d.shift ? d.shift[nn] : 0.0f);
       if (d.res1) x += d.res1[m * d.ldr1 + nn];
+      if (d.res1_bf16) x += bf16_lo(d.res1_bf16[m * d.ldr1 + nn]);
       x = act_apply(x, d.act);
       if (d.res2) x += d.res2[m * d.ldr2 + nn];
-      crow[nn] = x;
+      if (d.C_bf16) d.C_bf16[ro + nn] = (uint16_t)(pack_bf16x2(x, 0.f) & 0xffffu);
+      else d.C[ro + nn] = x;
     }
   }
 }
@@ -170,9 +202,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         const int col = (cidx - row * (WN / 4)) * 4;
         const int64_t m = mr + row;
         const int n = nb + col;
-        r1[u] = (fastv && d.res1 && m < p.M && n < d.Cout)
-                    ? *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n)
-                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        r1[u] = (fastv && has_res1(d) && m < p.M && n < d.Cout) ? load_res1(d, m, n) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {

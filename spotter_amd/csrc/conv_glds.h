@@ -340,10 +340,10 @@ __device__ __forceinline__ void glds_zero(f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M
 // Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
 // Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
 // index within that member.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int APL>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, int wg, f32x16 (&acc)[TM][TN],
                                               f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
-  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK>;
+  using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;  // the kernel's own LDS size decides the band count
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int wm = wave / WN;
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   ConvArgs q = p;
   q.d.C += (int64_t)bi * p.bs_c;
-  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16>(q, smem, wg, acc, acc4);
+  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16, APL>(q, smem, wg, acc, acc4);
 #if SP_GLDS_STAMP
   __syncthreads();
   GLDS_STAMP(3);
@@ -432,6 +432,7 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
   constexpr bool fit3a = AB && C3a::SMEM * 16 <= 163840, fit1a = AB && C1a::SMEM * 16 <= 163840;
   const bool a16 = a.A16 != nullptr;
+  if (a16 && !(planes == 3 ? fit3a : fit1a)) return -2;  // no bf16-A form of this tile: the caller picks another
   if ((planes == 3 && !(a16 ? fit3a : fit3)) || (planes != 3 && !(a16 ? fit1a : fit1))) {
     set_error("sp_conv2d: tile configuration not built for %d operand plane(s)%s (LDS or bf16-A variant)", planes,
               a16 ? " with bf16 A planes" : "");

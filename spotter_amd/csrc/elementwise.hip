@@ -73,6 +73,90 @@ __global__ __launch_bounds__(256) void avgpool2_kernel(const float4* __restrict_
   }
 }
 
+// bf16 rows (the bf16 variant's backbone maps, ABI v10): 8 channels (16 bytes) per thread, same 2-D grid.
+__device__ __forceinline__ void unpack8(const uint4 u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __builtin_bit_cast(float, w[i] << 16);
+    f[2 * i + 1] = __builtin_bit_cast(float, w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(pk_bf16(f[0], f[1]), pk_bf16(f[2], f[3]), pk_bf16(f[4], f[5]), pk_bf16(f[6], f[7]));
+}
+
+__global__ __launch_bounds__(256) void maxpool3s2_bf16_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
+                                                              int n, int h, int w, int c8, int ho, int wo,
+                                                              int64_t ldy8) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= wo * c8) return;
+  const int ox = j / c8, cc = j - ox * c8;
+  for (int row = blockIdx.y; row < n * ho; row += gridDim.y) {
+    const int oy = row % ho, b = row / ho;
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = oy * 2 - 1 + dy;
+      if ((unsigned)iy >= (unsigned)h) continue;
+      const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ix = ox * 2 - 1 + dx;
+        if ((unsigned)ix >= (unsigned)w) continue;
+        float f[8];
+        unpack8(xr[ix * c8], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
+      }
+    }
+    y[((int64_t)row * wo + ox) * ldy8 + cc] = pack8(m);  // exact: every max is a bf16 value
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool2_bf16_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
+                                                            int n, int h, int w, int c8, int ho, int wo,
+                                                            int64_t ldy8) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= wo * c8) return;
+  const int ox = j / c8, cc = j - ox * c8;
+  for (int row = blockIdx.y; row < n * ho; row += gridDim.y) {
+    const int oy = row % ho, b = row / ho;
+    float s[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] = 0.f;
+    int cnt = 0;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int iy = oy * 2 + dy;
+      if (iy >= h) continue;
+      const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        const int ix = ox * 2 + dx;
+        if (ix >= w) continue;
+        float f[8];
+        unpack8(xr[ix * c8], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s[e] += f[e];
+        ++cnt;
+      }
+    }
+    const float inv = (float)cnt;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] /= inv;
+    y[((int64_t)row * wo + ox) * ldy8 + cc] = pack8(s);
+  }
+}
+
 __global__ void upsample2_kernel(const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
                                  int64_t ldy, int n, int h, int w, int c4) {
   const int ho = 2 * h, wo = 2 * w;
@@ -258,6 +342,32 @@ extern "C" int sp_avgpool2x2_ceil(const float* x, float* y, int64_t ldy, int n, 
   hipLaunchKernelGGL(avgpool2_kernel, dim3((wo * (c / 4) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
                      (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4);
   return check_launch("sp_avgpool2x2_ceil");
+}
+
+extern "C" int sp_maxpool3x3s2_bf16(const uint16_t* x, uint16_t* y, int64_t ldy, int n, int h, int w, int c,
+                                    void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && ldy >= c && ldy % 8 == 0 &&
+                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)x & 15) == 0,
+               "sp_maxpool3x3s2_bf16: bad args");
+  int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  SP_ARG_CHECK((int64_t)n * ho < (1 << 30) && (int64_t)wo * (c / 8) < (1 << 30), "sp_maxpool3x3s2_bf16: size out of range");
+  const int gy = n * ho < 65535 ? n * ho : 65535;
+  hipLaunchKernelGGL(maxpool3s2_bf16_kernel, dim3((wo * (c / 8) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
+                     (const uint4*)x, (uint4*)y, n, h, w, c / 8, ho, wo, ldy / 8);
+  return check_launch("sp_maxpool3x3s2_bf16");
+}
+
+extern "C" int sp_avgpool2x2_ceil_bf16(const uint16_t* x, uint16_t* y, int64_t ldy, int n, int h, int w, int c,
+                                       void* stream) {
+  SP_ARG_CHECK(x && y && n > 0 && h > 0 && w > 0 && c > 0 && c % 8 == 0 && ldy >= c && ldy % 8 == 0 &&
+                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)x & 15) == 0,
+               "sp_avgpool2x2_ceil_bf16: bad args");
+  int ho = (h + 1) / 2, wo = (w + 1) / 2;
+  SP_ARG_CHECK((int64_t)n * ho < (1 << 30) && (int64_t)wo * (c / 8) < (1 << 30), "sp_avgpool2x2_ceil_bf16: size out of range");
+  const int gy = n * ho < 65535 ? n * ho : 65535;
+  hipLaunchKernelGGL(avgpool2_bf16_kernel, dim3((wo * (c / 8) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
+                     (const uint4*)x, (uint4*)y, n, h, w, c / 8, ho, wo, ldy / 8);
+  return check_launch("sp_avgpool2x2_ceil_bf16");
 }
 
 extern "C" int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, int n, int h,

@@ -18,10 +18,18 @@ constexpr int STEM_BLOCK = 256;
 // Each lane computes one pixel's CO outputs; the workgroup's 256 consecutive NHWC rows are one
 // contiguous span of y, so the results are staged in LDS (row stride CO+4 floats: 16-byte aligned,
 // rows spread over the banks) and written back as consecutive float4s across the lanes.
-template <int CO>
+// OT: float (fp32 rows) or uint16_t (bf16 rows, RNE at the store: the bf16 variant, ABI v10).
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
+}
+
+template <int CO, typename OT>
 __global__ __launch_bounds__(STEM_BLOCK) void stem_conv_nchw_kernel(
     const float* __restrict__ x, const float* __restrict__ wt, const float* __restrict__ scale,
-    const float* __restrict__ shift, float* __restrict__ y, int n, int h, int w, int ho, int wo,
+    const float* __restrict__ shift, OT* __restrict__ y, int n, int h, int w, int ho, int wo,
     int relu) {
   constexpr int LD = CO + 4;
   __shared__ float4 tile4[STEM_BLOCK * LD / 4];
@@ -73,11 +81,20 @@ __global__ __launch_bounds__(STEM_BLOCK) void stem_conv_nchw_kernel(
   }
   __syncthreads();
   constexpr int C4 = CO / 4;
-  float4* yo = reinterpret_cast<float4*>(y + p0 * CO);
   const int n4 = rows * C4;
-  for (int i = t; i < n4; i += STEM_BLOCK) {
-    const int r = i / C4, c = i - r * C4;
-    yo[i] = *reinterpret_cast<const float4*>(tile + r * LD + 4 * c);
+  if constexpr (sizeof(OT) == 4) {
+    float4* yo = reinterpret_cast<float4*>(y + p0 * CO);
+    for (int i = t; i < n4; i += STEM_BLOCK) {
+      const int r = i / C4, c = i - r * C4;
+      yo[i] = *reinterpret_cast<const float4*>(tile + r * LD + 4 * c);
+    }
+  } else {
+    uint2* yo = reinterpret_cast<uint2*>(y + p0 * CO);
+    for (int i = t; i < n4; i += STEM_BLOCK) {
+      const int r = i / C4, c = i - r * C4;
+      const float4 v = *reinterpret_cast<const float4*>(tile + r * LD + 4 * c);
+      yo[i] = make_uint2(pk_bf16(v.x, v.y), pk_bf16(v.z, v.w));
+    }
   }
 }
 
@@ -86,19 +103,34 @@ __global__ __launch_bounds__(STEM_BLOCK) void stem_conv_nchw_kernel(
 
 using namespace sp;
 
-extern "C" int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, const float* shift,
-                                      float* y, int n, int h, int w, int cout, int act, void* stream) {
+namespace sp {
+namespace {
+template <typename OT>
+int stem_launch(const char* what, const float* x, const float* wt, const float* scale, const float* shift, OT* y,
+                int n, int h, int w, int cout, int act, void* stream) {
   SP_ARG_CHECK(x && wt && scale && shift && y && n > 0 && h > 0 && w > 0 && (act == 0 || act == 1) &&
                    (cout == 32 || cout == 64),
-               "sp_stem_conv3x3s2_nchw: bad args (cout must be 32 or 64, act none/relu)");
+               "%s: bad args (cout must be 32 or 64, act none/relu)", what);
   const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const int64_t total = (int64_t)n * ho * wo;
   const unsigned grid = (unsigned)((total + STEM_BLOCK - 1) / STEM_BLOCK);
   if (cout == 32)
-    hipLaunchKernelGGL(stem_conv_nchw_kernel<32>, dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt, scale,
-                       shift, y, n, h, w, ho, wo, act);
+    hipLaunchKernelGGL((stem_conv_nchw_kernel<32, OT>), dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt,
+                       scale, shift, y, n, h, w, ho, wo, act);
   else
-    hipLaunchKernelGGL(stem_conv_nchw_kernel<64>, dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt, scale,
-                       shift, y, n, h, w, ho, wo, act);
-  return check_launch("sp_stem_conv3x3s2_nchw");
+    hipLaunchKernelGGL((stem_conv_nchw_kernel<64, OT>), dim3(grid), dim3(STEM_BLOCK), 0, as_stream(stream), x, wt,
+                       scale, shift, y, n, h, w, ho, wo, act);
+  return check_launch(what);
+}
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, const float* shift,
+                                      float* y, int n, int h, int w, int cout, int act, void* stream) {
+  return stem_launch("sp_stem_conv3x3s2_nchw", x, wt, scale, shift, y, n, h, w, cout, act, stream);
+}
+
+extern "C" int sp_stem_conv3x3s2_nchw_bf16(const float* x, const float* wt, const float* scale, const float* shift,
+                                           uint16_t* y, int n, int h, int w, int cout, int act, void* stream) {
+  return stem_launch("sp_stem_conv3x3s2_nchw_bf16", x, wt, scale, shift, y, n, h, w, cout, act, stream);
 }

@@ -150,7 +150,8 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False):
+                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False,
+                 bf16_store: bool | None = None):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -191,6 +192,12 @@ class Engine:
         self.act_aifi = cfg.encoder_activation_function
         self.act_dec = cfg.decoder_activation_function
         self._conv_mode, self._lin_mode = PRECISIONS[precision]
+        # bf16 conv operands: keep the backbone's activation maps in HBM as bf16 rows (half the bytes of every
+        # producer write and consumer read; the GEMMs stage them as their bf16 A plane, the epilogues round
+        # once at the store) instead of fp32 maps rounded per GEMM fragment. Default on for the bf16 modes.
+        self.bf16_store = (self._conv_mode == "bf16") if bf16_store is None else bool(bf16_store)
+        if self.bf16_store and self._conv_mode != "bf16":
+            raise ValueError("bf16_store needs a bf16 conv operand mode")
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -436,7 +443,7 @@ class Engine:
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        if cw.wino is not None and stride == 1 and not kw and self._wino_pays(n * h * w, cw.cin):
+        if cw.wino is not None and stride == 1 and not kw and not x.is_bf16 and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
             vpl = self.wino_v_planes and wm == 4 and cw.wino.shape[0] == 3
@@ -481,9 +488,14 @@ class Engine:
         pixel_values is the processor's NCHW batch (IPP:461-462)."""
         e = self.cfg.embedding_size
         h1, w1 = (H - 1) // 2 + 1, (W - 1) // 2 + 1
-        s0 = self._buf("stem0", B, h1, w1, e // 2)
-        s1 = self._buf("stem1", B, h1, w1, e // 2)
-        s2 = self._buf("stem2", B, h1, w1, e)
+        dt = torch.int16 if self.bf16_store else torch.float32  # bf16 maps: bit patterns in int16 buffers
+
+        def buf(key, *shape):
+            return self._buf(key, *shape, dtype=dt)
+
+        s0 = buf("stem0", B, h1, w1, e // 2)
+        s1 = buf("stem1", B, h1, w1, e // 2)
+        s2 = buf("stem2", B, h1, w1, e)
         c0 = self.stem[0]
         if self._direct_stem():
             ops.stem_conv_nchw(pixel_values, c0.w, c0.scale, c0.shift, view(s0, e // 2), c0.cout, act=self.act_bb)
@@ -498,9 +510,9 @@ class Engine:
         if "fused" in b0 and b0["sc"] == "conv":
             # the first block's fused tail reads the pooled stem next to its conv2 output: pool into that slice
             kc = b0["layers"][0].cout + e
-            curv = V(self._buf(f"s{b0['s']}_cat", B, h, w, kc), kc - e, kc)
+            curv = V(buf(f"s{b0['s']}_cat", B, h, w, kc), kc - e, kc)
         else:
-            curv = view(self._buf("pool", B, h, w, e), e)
+            curv = view(buf("pool", B, h, w, e), e)
         ops.maxpool3x3s2(s2, curv, B, h1, w1, e)
         c = e
         feats = []
@@ -518,13 +530,13 @@ class Engine:
                 kc = red + c
                 if blk["sc"] == "avgconv":
                     assert curv.off == 0 and curv.ld == c
-                    cat = self._buf(f"s{s}_cat", B, ho, wo, kc)
+                    cat = buf(f"s{s}_cat", B, ho, wo, kc)
                     ops.avgpool2x2_ceil(cur, V(cat, red, kc), B, h, w, c)
                 else:  # stride-1 projection: the block input already sits in the slice (see above)
                     assert curv.off == red and curv.ld == kc and st == 1
                     cat = cur
-                t1 = self._buf(f"s{s}_t1", B, h, w, red)
-                out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
+                t1 = buf(f"s{s}_t1", B, h, w, red)
+                out = buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
                 self._cv(curv, B, h, w, L[0], 1, view(t1, red), act=self.act_bb)
                 self._cv(view(t1, red), B, h, w, L[1], st, V(cat, 0, kc), act=self.act_bb)
                 self._cv(V(cat, 0, kc), B, ho, wo, blk["fused"], 1, view(out, cout), act=self.act_bb)
@@ -537,22 +549,22 @@ class Engine:
             else:
                 src, sh_, sw_ = cur, h, w
                 if blk["sc"] == "avgconv":
-                    pooled = self._buf(f"s{s}_pool", B, (h + 1) // 2, (w + 1) // 2, c)
+                    pooled = buf(f"s{s}_pool", B, (h + 1) // 2, (w + 1) // 2, c)
                     ops.avgpool2x2_ceil(cur, pooled, B, h, w, c)
                     src, sh_, sw_ = pooled, (h + 1) // 2, (w + 1) // 2
-                sbuf = self._buf(f"s{s}_sc", B, ho, wo, cout)
+                sbuf = buf(f"s{s}_sc", B, ho, wo, cout)
                 self._cv(view(src, c), B, sh_, sw_, blk["short"], 1 if blk["sc"] == "avgconv" else st, view(sbuf, cout))
                 res = view(sbuf, cout)
-            out = self._buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
+            out = buf(f"s{s}_out{i % 2}", B, ho, wo, cout)
             if blk["type"] == "bottleneck":
                 red = L[0].cout
-                t1 = self._buf(f"s{s}_t1", B, h, w, red)
-                t2 = self._buf(f"s{s}_t2", B, ho, wo, red)
+                t1 = buf(f"s{s}_t1", B, h, w, red)
+                t2 = buf(f"s{s}_t2", B, ho, wo, red)
                 self._cv(view(cur, c), B, h, w, L[0], 1, view(t1, red), act=self.act_bb)
                 self._cv(view(t1, red), B, h, w, L[1], st, view(t2, red), act=self.act_bb)
                 self._cv(view(t2, red), B, ho, wo, L[2], 1, view(out, cout), act=self.act_bb, res1=res)
             else:
-                t1 = self._buf(f"s{s}_t1", B, ho, wo, cout)
+                t1 = buf(f"s{s}_t1", B, ho, wo, cout)
                 self._cv(view(cur, c), B, h, w, L[0], st, view(t1, cout), act=self.act_bb)
                 self._cv(view(t1, cout), B, ho, wo, L[1], 1, view(out, cout), act=self.act_bb, res1=res)
             curv, h, w, c = view(out, cout), ho, wo, cout

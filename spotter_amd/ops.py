@@ -42,18 +42,25 @@ def stream() -> int:
 
 @dataclass
 class V:
-    """A strided row view into a float32 device tensor: rows of `ld` elements from `off`."""
+    """A strided row view into a device tensor: rows of `ld` elements from `off`. float32 rows, or bf16 rows
+    held as int16 bit patterns (the bf16 variant's backbone maps, `is_bf16`)."""
     t: torch.Tensor
     off: int = 0
     ld: int = 0
 
     @property
-    def ptr(self) -> int:
-        return self.t.data_ptr() + 4 * self.off
+    def is_bf16(self) -> bool:
+        return self.t.dtype == torch.int16
 
-    def need(self, rows: int, cols: int, what: str):
-        if self.t.dtype != torch.float32 or not self.t.is_cuda:
-            raise TypeError(f"{what}: expected a float32 CUDA tensor")
+    @property
+    def ptr(self) -> int:
+        return self.t.data_ptr() + self.t.element_size() * self.off
+
+    def need(self, rows: int, cols: int, what: str, bf16: bool = False):
+        """Checked pointer to rows × cols; float32 rows unless bf16 (then int16 bit patterns)."""
+        want = torch.int16 if bf16 else torch.float32
+        if self.t.dtype != want or not self.t.is_cuda:
+            raise TypeError(f"{what}: expected a {'bf16 (int16)' if bf16 else 'float32'} CUDA tensor")
         if not self.t.is_contiguous():
             raise ValueError(f"{what}: tensor must be contiguous")
         last = self.off + (rows - 1) * self.ld + cols if rows > 0 else self.off
@@ -88,7 +95,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     wo = (w + 2 * pad - k) // stride + 1
     m = n * ho * wo
     d = SpConvDesc()
-    d.A = x.need(n * h * w, cin, "conv.A")
+    if x.is_bf16:  # bf16 activation rows: the GEMM stages them as its one bf16 A plane
+        d.A_bf16 = x.need(n * h * w, cin, "conv.A", bf16=True)
+    else:
+        d.A = x.need(n * h * w, cin, "conv.A")
     d.lda = x.ld
     if a_bf16 is not None:
         a16, aps = a_bf16
@@ -115,7 +125,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         d.row_scale = row_scale.data_ptr()
         d.row_period = row_scale.numel()
     if res1 is not None:
-        d.res1 = res1.need(m, cout, "conv.res1")
+        if res1.is_bf16:
+            d.res1_bf16 = res1.need(m, cout, "conv.res1", bf16=True)
+        else:
+            d.res1 = res1.need(m, cout, "conv.res1")
         d.ldr1 = res1.ld
     d.act = ACT[act]
     if res2 is not None:
@@ -127,6 +140,8 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         if last > out.t.numel() or cout > out.ld:
             raise ValueError("conv.C grouped span exceeds output")
         d.C = out.ptr
+    elif out.is_bf16:  # bf16 output rows (RNE in the epilogue)
+        d.C_bf16 = out.need(m, cout, "conv.C", bf16=True)
     else:
         d.C = out.need(m, cout, "conv.C")
     d.ldc = out.ld
@@ -157,8 +172,12 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
         d.workspace_elems = workspace.numel()
-    nbytes = 4 * (n * h * w * cin * (2 if a2 is not None else 1) + cout * k * k * cin + m * cout
-                  * (1 + (res1 is not None) + (res2 is not None)))
+    # compulsory bytes: activations at their storage width (fp32 or bf16 rows), weights in the operand form
+    # the GEMM streams (fp32, one bf16 plane, or the three split planes)
+    wbytes = 2 if wt16 is not None else 6 if wt_planes is not None else 4
+    nbytes = (x.t.element_size() * n * h * w * cin + 4 * n * h * w * cin * (a2 is not None)
+              + wbytes * cout * k * k * cin + m * cout * (out.t.element_size()
+              + (res1.t.element_size() if res1 is not None else 0) + 4 * (res2 is not None)))
     if wino is not None:
         planes, work = wino[0], wino[1]
         wm = wino[2] if len(wino) > 2 else 2
@@ -292,40 +311,44 @@ def stem_conv_nchw(x: torch.Tensor, wt: torch.Tensor, scale: torch.Tensor, shift
         raise ValueError("stem_conv_nchw: weight / affine size mismatch")
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     m = n * ho * wo
-    yp = y.need(m, cout, "stem.y")
-    _launch("conv", "sp_stem_conv3x3s2_nchw",
+    yp = y.need(m, cout, "stem.y", bf16=y.is_bf16)  # bf16 rows: the bf16 variant's backbone (RNE at the store)
+    _launch("conv", "sp_stem_conv3x3s2_nchw" + ("_bf16" if y.is_bf16 else ""),
             (x.data_ptr(), wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, n, h, w, cout, ACT[act],
-             stream()), 2 * m * cout * 27, 4 * (x.numel() + cout * 27 + m * cout), (m, cout, 27, 3, 2, "direct"))
+             stream()), 2 * m * cout * 27, 4 * (x.numel() + cout * 27) + y.t.element_size() * m * cout,
+            (m, cout, 27, 3, 2, "direct"))
     return ho, wo
 
 
 def _pool_out(y, m: int, c: int, what: str):
     """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
     if isinstance(y, V):
-        if y.ld % 4 or y.off % 4:
-            raise ValueError(f"{what}: output view must be float4-aligned")
-        return y.need(m, c, what), y.ld
+        if y.ld % 4 or y.off % 4 or (y.is_bf16 and (y.ld % 8 or y.off % 8)):
+            raise ValueError(f"{what}: output view must be 16-byte aligned")
+        return y.need(m, c, what, bf16=y.is_bf16), y.ld
     if y.numel() < m * c:
         raise ValueError(f"{what}: output too small")
     return y.data_ptr(), c
 
 
-def maxpool3x3s2(x: torch.Tensor, y, n, h, w, c):
-    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+def _pool(name, x: torch.Tensor, y, n, h, w, c, ho, wo):
+    """float32 rows, or bf16 rows (int16 x and y: the *_bf16 kernels)."""
     assert x.numel() >= n * h * w * c
-    yp, ldy = _pool_out(y, n * ho * wo, c, "maxpool.y")
-    _launch("elementwise", "sp_maxpool3x3s2", (x.data_ptr(), yp, ldy, n, h, w, c, stream()), 0,
-            4 * n * c * (h * w + ho * wo))
+    bf = x.dtype == torch.int16
+    yv = y if isinstance(y, V) else view(y, c)
+    if yv.is_bf16 != bf:
+        raise TypeError(f"{name}: input and output rows must both be float32 or both bf16")
+    yp, ldy = _pool_out(y, n * ho * wo, c, name + ".y")
+    _launch("elementwise", name + ("_bf16" if bf else ""), (x.data_ptr(), yp, ldy, n, h, w, c, stream()), 0,
+            x.element_size() * n * c * (h * w + ho * wo))
     return ho, wo
+
+
+def maxpool3x3s2(x: torch.Tensor, y, n, h, w, c):
+    return _pool("sp_maxpool3x3s2", x, y, n, h, w, c, (h - 1) // 2 + 1, (w - 1) // 2 + 1)
 
 
 def avgpool2x2_ceil(x: torch.Tensor, y, n, h, w, c):
-    ho, wo = (h + 1) // 2, (w + 1) // 2
-    assert x.numel() >= n * h * w * c
-    yp, ldy = _pool_out(y, n * ho * wo, c, "avgpool.y")
-    _launch("elementwise", "sp_avgpool2x2_ceil", (x.data_ptr(), yp, ldy, n, h, w, c, stream()), 0,
-            4 * n * c * (h * w + ho * wo))
-    return ho, wo
+    return _pool("sp_avgpool2x2_ceil", x, y, n, h, w, c, (h + 1) // 2, (w + 1) // 2)
 
 
 def upsample2x(x: V, y: V, n, h, w, c):

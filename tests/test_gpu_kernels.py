@@ -365,7 +365,7 @@ def test_conv2d_bf16_a_planes_bit_identical(dev):
             a16 = T(np.ascontiguousarray(pl).reshape(-1).view(np.int16), dev)
             wkw = dict(wt_planes=ops.split_bf16x3(wk)) if mode == "x3" else dict(
                 wt16=T(ops.bf16_bits(wt).view(np.int16), dev))
-            for cfg in (None, "14", "46", "45", "12", "33", "47", "63", "16"):
+            for cfg in (None, "14", "46", "45", "12", "33", "47", "63", "16", "51", "41", "44", "64", "13"):  # (42: no split-A-plane form fits the LDS)
                 outs = []
                 for use16 in (False, True):
                     out = torch.full((n * ho * wo * cout,), float("nan"), device=dev)
@@ -385,6 +385,80 @@ def test_conv2d_bf16_a_planes_bit_identical(dev):
                     assert cfg is not None, outs  # only a forced tile may lack the form
                     continue
                 assert np.array_equal(outs[0], outs[1]), (mode, cfg, k, np.abs(outs[0] - outs[1]).max())
+
+
+def _bf16_rows(a):
+    """fp32 array → (int16 bf16 bit patterns, their exact fp32 values)."""
+    from spotter_amd import ops
+
+    bits = ops.bf16_bits(a)
+    return bits.view(np.int16), ops._bf16_float(bits)
+
+
+@pytest.mark.parametrize("k,stride,cfg", [(1, 1, None), (3, 2, None), (3, 1, "14"), (1, 1, "45"), (1, 1, "12"),
+                                          (3, 1, "51"), (3, 2, "41"), (3, 1, "64"), (1, 1, "33"), (3, 1, "16")])
+def test_conv2d_bf16_rows_in_and_out(dev, k, stride, cfg):
+    """bf16 activation rows (ABI v10, the bf16 variant's backbone): A_bf16 in, res1_bf16, C_bf16 out (into a
+    channel slice of a wider buffer) equal the fp32-row launch on the same bf16-representable values with
+    its fp32 output rounded to bf16 (RNE) — bit for bit."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(31 + k + stride)
+    n, h, w, cin, cout = 2, 11, 14, 64, 96
+    ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (w + 2 * (k // 2) - k) // stride + 1
+    m = n * ho * wo
+    x16, x32 = _bf16_rows(rng.standard_normal((n * h * w, cin)).astype(np.float32))
+    r16, r32 = _bf16_rows(rng.standard_normal((m, cout)).astype(np.float32))
+    wt = (rng.standard_normal((cout, k * k * cin)) / np.sqrt(k * k * cin)).astype(np.float32)
+    wk = T(wt, dev)
+    w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
+    sc, sh = T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev), T(rng.standard_normal(cout).astype(np.float32), dev)
+    ops.force_conv_config(cfg)
+    try:
+        ref = torch.empty(m * cout, device=dev)
+        ops.conv2d(V(T(x32.reshape(-1), dev), 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2, V(ref, 0, cout),
+                   scale=sc, shift=sh, act="relu", res1=V(T(r32.reshape(-1), dev), 0, cout), wt16=w16)
+        out = torch.full((m * (cout + 16),), -1, dtype=torch.int16, device=dev)
+        ops.conv2d(V(T(x16.reshape(-1), dev), 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2,
+                   V(out, 8, cout + 16), scale=sc, shift=sh, act="relu", res1=V(T(r16.reshape(-1), dev), 0, cout),
+                   wt16=w16)
+    finally:
+        ops.force_conv_config(None)
+    want = ops.bf16_bits(ref.cpu().numpy()).view(np.int16).reshape(m, cout)
+    got = out.cpu().numpy().reshape(m, cout + 16)
+    assert np.array_equal(got[:, 8:8 + cout], want)
+    assert np.all(got[:, :8] == -1) and np.all(got[:, 8 + cout:] == -1)
+
+
+def test_pools_and_stem_bf16_rows(dev):
+    """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32
+    kernels on the same bf16-representable inputs with the result rounded to bf16 (max: exact)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(41)
+    n, h, w, c = 2, 13, 10, 64
+    x16, x32 = _bf16_rows(rng.standard_normal((n * h * w, c)).astype(np.float32))
+    for fn, (ho, wo) in ((ops.maxpool3x3s2, ((h - 1) // 2 + 1, (w - 1) // 2 + 1)),
+                         (ops.avgpool2x2_ceil, ((h + 1) // 2, (w + 1) // 2))):
+        ref = torch.empty(n * ho * wo * c, device=dev)
+        fn(T(x32.reshape(-1), dev), ref, n, h, w, c)
+        out = torch.full((n * ho * wo * (c + 8),), -1, dtype=torch.int16, device=dev)
+        fn(T(x16.reshape(-1), dev), V(out, 8, c + 8), n, h, w, c)
+        want = ops.bf16_bits(ref.cpu().numpy()).view(np.int16).reshape(-1, c)
+        got = out.cpu().numpy().reshape(-1, c + 8)
+        assert np.array_equal(got[:, 8:], want), fn.__name__
+        assert np.all(got[:, :8] == -1)
+    px = T(rng.uniform(0, 1, (2, 3, 37, 30)).astype(np.float32), dev)
+    wt = T((rng.standard_normal((32, 27)) / 5).astype(np.float32), dev)
+    sc, sh = T(rng.uniform(0.5, 1.5, 32).astype(np.float32), dev), T(rng.standard_normal(32).astype(np.float32), dev)
+    m = 2 * 19 * 15
+    ref = torch.empty(m * 32, device=dev)
+    ops.stem_conv_nchw(px, wt, sc, sh, V(ref, 0, 32), 32, act="relu")
+    out = torch.empty(m * 32, dtype=torch.int16, device=dev)
+    ops.stem_conv_nchw(px, wt, sc, sh, V(out, 0, 32), 32, act="relu")
+    assert np.array_equal(out.cpu().numpy(), ops.bf16_bits(ref.cpu().numpy()).view(np.int16))
 
 
 def test_conv2d_f32x3_epilogue_and_views(dev):

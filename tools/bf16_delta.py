@@ -89,7 +89,7 @@ def ap_vs_fp32(out, g, proc):
     return {"map": r["map"], "ap50": r["ap50"], "ap75": r["ap75"]}
 
 
-def delta(preset, tag=None, precision="bf16", reps=1):
+def delta(preset, tag=None, precision="bf16", reps=1, **ekw):
     """The golden images (tiled `reps` times into one batch) through Engine(precision) → agreement
     with the fp32 goldens at threshold 0.5 and the AP of the ranked candidates."""
     from tests.test_gpu_model import load_images
@@ -100,7 +100,7 @@ def delta(preset, tag=None, precision="bf16", reps=1):
     g = np.load(os.path.join(GOLD, f"{tag or preset + '_640'}.npz"))
     size = int(g["size"])
     model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False)
-    model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision)
+    model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision, **ekw)
     proc = SpotterImageProcessor(size={"height": size, "width": size})
     imgs = load_images(g) * reps
     with torch.no_grad():
@@ -120,9 +120,12 @@ if __name__ == "__main__":
     ap.add_argument("precision", nargs="?", default="bf16")
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--fp32-maps", action="store_true", help="bf16 modes: fp32 backbone maps (Engine bf16_store=False)")
     a = ap.parse_args()
-    res = {p: delta(p, precision=a.precision, reps=a.reps) for p in ("r18vd", "r101vd")}
+    ekw = {"bf16_store": False} if a.fp32_maps else {}
+    res = {p: delta(p, precision=a.precision, reps=a.reps, **ekw) for p in ("r18vd", "r101vd")}
     res["precision"] = a.precision
+    res["backbone_maps"] = "fp32" if a.fp32_maps else ("bf16" if a.precision.startswith("bf16") else "fp32")
     line = json.dumps({"metric": "bf16 variant delta vs HF fp32 goldens (synthetic weights; COCO-val unpinned)",
                        **res})
     print(line)
