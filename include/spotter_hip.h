@@ -108,9 +108,11 @@ typedef struct {
   int32_t wino_v_planes;
   /* ABI v10: bf16 activations (the bf16 variant keeps the backbone's maps in bf16). C_bf16 (non-NULL)
    * replaces C: the epilogue result is stored as bf16 (RNE) rows, ldc / out_group_stride in elements.
-   * res1_bf16 (non-NULL) replaces res1 (bf16 rows, ldr1 in elements). Not with LayerNorm. */
+   * res1_bf16 / res2_bf16 (non-NULL) replace res1 / res2 (bf16 rows, ldr1 / ldr2 in elements). Not with
+   * LayerNorm. */
   uint16_t* C_bf16;
   const uint16_t* res1_bf16;
+  const uint16_t* res2_bf16;
 } sp_conv_desc;
 
 /*

@@ -43,7 +43,7 @@ class SpConvDesc(C.Structure):
         ("precision", i32), ("Wt_bf16", vp), ("wt_plane_stride", i64),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
-        ("C_bf16", vp), ("res1_bf16", vp),
+        ("C_bf16", vp), ("res1_bf16", vp), ("res2_bf16", vp),
     ]
 
 

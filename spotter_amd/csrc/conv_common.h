@@ -97,6 +97,9 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
   if (d.res2) {
     const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
     v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  } else if (d.res2_bf16) {
+    const uint2 u = *reinterpret_cast<const uint2*>(d.res2_bf16 + m * d.ldr2 + n);
+    v.x += bf16_lo(u.x); v.y += bf16_hi(u.x); v.z += bf16_lo(u.y); v.w += bf16_hi(u.y);
   }
   store_out4(d, m, n, v);
 }
@@ -120,6 +123,7 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int
       if (d.res1_bf16) x += bf16_lo(d.res1_bf16[m * d.ldr1 + nn]);
       x = act_apply(x, d.act);
       if (d.res2) x += d.res2[m * d.ldr2 + nn];
+      if (d.res2_bf16) x += bf16_lo(d.res2_bf16[m * d.ldr2 + nn]);
       if (d.C_bf16) d.C_bf16[ro + nn] = (uint16_t)(pack_bf16x2(x, 0.f) & 0xffffu);
       else d.C[ro + nn] = x;
     }

@@ -294,7 +294,8 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   using namespace sp;
   SP_ARG_CHECK(d != nullptr, "sp_conv2d: null descriptor");
   SP_ARG_CHECK((d->A || d->A_bf16) && d->Wt && (d->C || d->C_bf16), "sp_conv2d: null A/W/C");
-  SP_ARG_CHECK(!(d->res1 && d->res1_bf16) && !(d->ln_gamma && (d->C_bf16 || d->res1_bf16)),
+  SP_ARG_CHECK(!(d->res1 && d->res1_bf16) && !(d->res2 && d->res2_bf16) &&
+                   !(d->ln_gamma && (d->C_bf16 || d->res1_bf16 || d->res2_bf16)),
                "sp_conv2d: res1 and res1_bf16 together, or bf16 rows with the fused LayerNorm");
   SP_ARG_CHECK(d->N > 0 && d->H > 0 && d->W > 0 && d->Cin > 0 && d->Cout > 0,
                "sp_conv2d: bad shape N=%d H=%d W=%d Cin=%d Cout=%d", d->N, d->H, d->W, d->Cin,
@@ -342,6 +343,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     bool v = (d->ldc % 4 == 0) && (d->C_bf16 ? al8(d->C_bf16) : al16(d->C)) && (d->Cout % 4 == 0);
     v = v && (!d->res1 || (d->ldr1 % 4 == 0 && al16(d->res1)));
     v = v && (!d->res1_bf16 || (d->ldr1 % 4 == 0 && al8(d->res1_bf16)));
+    v = v && (!d->res2_bf16 || (d->ldr2 % 4 == 0 && al8(d->res2_bf16)));
     v = v && (!d->res2 || (d->ldr2 % 4 == 0 && al16(d->res2)));
     v = v && (!d->scale || al16(d->scale)) && (!d->shift || al16(d->shift));
     v = v && (d->out_rows_per_group == 0 || d->out_group_stride % 4 == 0);

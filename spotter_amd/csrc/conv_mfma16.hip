@@ -1387,7 +1387,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
-  if (cfg >= 70 && cfg <= 75 && (a.d.C_bf16 || a.d.res1_bf16)) cfg = -1;  // register epilogues: fp32 rows only
+  if (cfg >= 70 && cfg <= 75 && (a.d.C_bf16 || a.d.res1_bf16 || a.d.res2_bf16)) cfg = -1;  // register epilogues: fp32 rows only
   if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1 && a.vec_epi) {
     switch (cfg) {
       case 73: return launch_x3p<8>(a, planes, s);  // 256×256 persistent

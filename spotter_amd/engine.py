@@ -575,18 +575,19 @@ class Engine:
     def _csp_fwd(self, cs, x: V, B, h, w, out: V, tag):
         """RTDetrV2CSPRepLayer.forward M2:948-952 on a 2·H-channel NHWC input."""
         hid = cs["hid"]
-        c12 = self._buf(f"{tag}_c12", B, h, w, 2 * hid)
+        dt = torch.int16 if self.bf16_store else torch.float32  # the bf16 variant keeps the CCFM maps in bf16
+        c12 = self._buf(f"{tag}_c12", B, h, w, 2 * hid, dtype=dt)
         self._cv(x, B, h, w, cs["c12"], 1, view(c12, 2 * hid), act=self.act_enc)
         h2 = V(c12, hid, 2 * hid)
         cur = V(c12, 0, 2 * hid)
-        t = None if self.fold_repvgg else self._buf(f"{tag}_t", B, h, w, hid)
+        t = None if self.fold_repvgg else self._buf(f"{tag}_t", B, h, w, hid, dtype=dt)
         final_to_out = cs["c3"] is None
         for b, (k3, k1) in enumerate(cs["reps"]):
             last = b == len(cs["reps"]) - 1
             if last and final_to_out:
                 dst = out
             else:
-                dst = view(self._buf(f"{tag}_r{b % 2}", B, h, w, hid), hid)
+                dst = view(self._buf(f"{tag}_r{b % 2}", B, h, w, hid, dtype=dt), hid)
             if k3 == "fold":
                 self._cv(cur, B, h, w, k1, 1, dst, act=self.act_enc, res2=h2 if last else None)
             else:
@@ -601,10 +602,13 @@ class Engine:
         cfg = self.cfg
         Hd = cfg.encoder_hidden_dim
         (f0, h0, w0, c0), (f1, h1, w1, c1), (f2, h2, w2, c2) = feats
-        cat3 = self._buf("cat3", B, h0, w0, 2 * Hd)   # [up(lat1) | proj0]
-        cat4 = self._buf("cat4", B, h1, w1, 2 * Hd)   # [up(lat0) | proj1]
-        catn4 = self._buf("catn4", B, h1, w1, 2 * Hd)  # [down0 | lat1]
-        catn5 = self._buf("catn5", B, h2, w2, 2 * Hd)  # [down1 | lat0]
+        # bf16 variant: the CCFM maps (concat buffers, CSPRep internals and outputs) in bf16 like the backbone's;
+        # AIFI (p5 → p5a) and everything from source_flatten on stay fp32
+        dt = torch.int16 if self.bf16_store else torch.float32
+        cat3 = self._buf("cat3", B, h0, w0, 2 * Hd, dtype=dt)   # [up(lat1) | proj0]
+        cat4 = self._buf("cat4", B, h1, w1, 2 * Hd, dtype=dt)   # [up(lat0) | proj1]
+        catn4 = self._buf("catn4", B, h1, w1, 2 * Hd, dtype=dt)  # [down0 | lat1]
+        catn5 = self._buf("catn5", B, h2, w2, 2 * Hd, dtype=dt)  # [down1 | lat0]
         p5 = self._buf("p5", B, h2, w2, Hd)
         self._cv(view(f0, c0), B, h0, w0, self.in_proj[0], 1, V(cat3, Hd, 2 * Hd))
         self._cv(view(f1, c1), B, h1, w1, self.in_proj[1], 1, V(cat4, Hd, 2 * Hd))
@@ -634,21 +638,21 @@ class Engine:
         # FPN (M2:1183-1197)
         self._cv(view(p5a, Hd), B, h2, w2, self.lateral[0], 1, V(catn5, Hd, 2 * Hd), act=self.act_enc)
         ops.upsample2x(V(catn5, Hd, 2 * Hd), V(cat4, 0, 2 * Hd), B, h2, w2, Hd)
-        F4 = self._buf("F4", B, h1, w1, Hd)
+        F4 = self._buf("F4", B, h1, w1, Hd, dtype=dt)
         self._csp_fwd(self.fpn[0], view(cat4, 2 * Hd), B, h1, w1, view(F4, Hd), "fpn0")
         yield
         self._cv(view(F4, Hd), B, h1, w1, self.lateral[1], 1, V(catn4, Hd, 2 * Hd), act=self.act_enc)
         ops.upsample2x(V(catn4, Hd, 2 * Hd), V(cat3, 0, 2 * Hd), B, h1, w1, Hd)
-        F3 = self._buf("F3", B, h0, w0, Hd)
+        F3 = self._buf("F3", B, h0, w0, Hd, dtype=dt)
         self._csp_fwd(self.fpn[1], view(cat3, 2 * Hd), B, h0, w0, view(F3, Hd), "fpn1")
         yield
         # PAN (M2:1199-1207)
         self._cv(view(F3, Hd), B, h0, w0, self.down[0], 2, V(catn4, 0, 2 * Hd), act=self.act_enc)
-        N4 = self._buf("N4", B, h1, w1, Hd)
+        N4 = self._buf("N4", B, h1, w1, Hd, dtype=dt)
         self._csp_fwd(self.pan[0], view(catn4, 2 * Hd), B, h1, w1, view(N4, Hd), "pan0")
         yield
         self._cv(view(N4, Hd), B, h1, w1, self.down[1], 2, V(catn5, 0, 2 * Hd), act=self.act_enc)
-        N5 = self._buf("N5", B, h2, w2, Hd)
+        N5 = self._buf("N5", B, h2, w2, Hd, dtype=dt)
         self._csp_fwd(self.pan[1], view(catn5, 2 * Hd), B, h2, w2, view(N5, Hd), "pan1")
         return [(F3, h0, w0), (N4, h1, w1), (N5, h2, w2)]
 

@@ -132,7 +132,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         d.ldr1 = res1.ld
     d.act = ACT[act]
     if res2 is not None:
-        d.res2 = res2.need(m, cout, "conv.res2")
+        if res2.is_bf16:
+            d.res2_bf16 = res2.need(m, cout, "conv.res2", bf16=True)
+        else:
+            d.res2 = res2.need(m, cout, "conv.res2")
         d.ldr2 = res2.ld
     if rows_per_group:
         groups = (m + rows_per_group - 1) // rows_per_group
@@ -177,7 +180,7 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     wbytes = 2 if wt16 is not None else 6 if wt_planes is not None else 4
     nbytes = (x.t.element_size() * n * h * w * cin + 4 * n * h * w * cin * (a2 is not None)
               + wbytes * cout * k * k * cin + m * cout * (out.t.element_size()
-              + (res1.t.element_size() if res1 is not None else 0) + 4 * (res2 is not None)))
+              + (res1.t.element_size() if res1 is not None else 0) + (res2.t.element_size() if res2 is not None else 0)))
     if wino is not None:
         planes, work = wino[0], wino[1]
         wm = wino[2] if len(wino) > 2 else 2
@@ -352,10 +355,18 @@ def avgpool2x2_ceil(x: torch.Tensor, y, n, h, w, c):
 
 
 def upsample2x(x: V, y: V, n, h, w, c):
-    xp = x.need(n * h * w, c, "upsample.x")
-    yp = y.need(n * 4 * h * w, c, "upsample.y")
-    _launch("elementwise", "sp_upsample2x_nearest", (xp, x.ld, yp, y.ld, n, h, w, c, stream()), 0,
-            4 * n * h * w * c * 5)
+    """Nearest ×2 upsample into a row view. bf16 rows (the bf16 variant's encoder maps) are a pure copy: the
+    same kernel moves them as float pairs (c / 2 "channels", row strides / 2)."""
+    bf = x.is_bf16
+    if y.is_bf16 != bf:
+        raise TypeError("upsample: input and output rows must both be float32 or both bf16")
+    xp = x.need(n * h * w, c, "upsample.x", bf16=bf)
+    yp = y.need(n * 4 * h * w, c, "upsample.y", bf16=bf)
+    if bf and (c % 8 or x.ld % 2 or y.ld % 2 or x.off % 2 or y.off % 2):
+        raise ValueError("upsample: bf16 rows need c % 8 == 0 and even strides / offsets")
+    k = 2 if bf else 1
+    _launch("elementwise", "sp_upsample2x_nearest", (xp, x.ld // k, yp, y.ld // k, n, h, w, c // k, stream()), 0,
+            x.t.element_size() * n * h * w * c * 5)
 
 
 def layernorm(x: V, gamma, beta, y: V, rows, d, eps=1e-5):

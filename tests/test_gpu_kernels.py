@@ -398,7 +398,7 @@ def _bf16_rows(a):
 @pytest.mark.parametrize("k,stride,cfg", [(1, 1, None), (3, 2, None), (3, 1, "14"), (1, 1, "45"), (1, 1, "12"),
                                           (3, 1, "51"), (3, 2, "41"), (3, 1, "64"), (1, 1, "33"), (3, 1, "16")])
 def test_conv2d_bf16_rows_in_and_out(dev, k, stride, cfg):
-    """bf16 activation rows (ABI v10, the bf16 variant's backbone): A_bf16 in, res1_bf16, C_bf16 out (into a
+    """bf16 activation rows (ABI v10, the bf16 variant's maps): A_bf16 in, res1_bf16, res2_bf16, C_bf16 out (into a
     channel slice of a wider buffer) equal the fp32-row launch on the same bf16-representable values with
     its fp32 output rounded to bf16 (RNE) — bit for bit."""
     from spotter_amd import ops
@@ -410,6 +410,7 @@ def test_conv2d_bf16_rows_in_and_out(dev, k, stride, cfg):
     m = n * ho * wo
     x16, x32 = _bf16_rows(rng.standard_normal((n * h * w, cin)).astype(np.float32))
     r16, r32 = _bf16_rows(rng.standard_normal((m, cout)).astype(np.float32))
+    q16, q32 = _bf16_rows(rng.standard_normal((m, cout)).astype(np.float32))
     wt = (rng.standard_normal((cout, k * k * cin)) / np.sqrt(k * k * cin)).astype(np.float32)
     wk = T(wt, dev)
     w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
@@ -418,11 +419,12 @@ def test_conv2d_bf16_rows_in_and_out(dev, k, stride, cfg):
     try:
         ref = torch.empty(m * cout, device=dev)
         ops.conv2d(V(T(x32.reshape(-1), dev), 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2, V(ref, 0, cout),
-                   scale=sc, shift=sh, act="relu", res1=V(T(r32.reshape(-1), dev), 0, cout), wt16=w16)
+                   scale=sc, shift=sh, act="relu", res1=V(T(r32.reshape(-1), dev), 0, cout),
+                   res2=V(T(q32.reshape(-1), dev), 0, cout), wt16=w16)
         out = torch.full((m * (cout + 16),), -1, dtype=torch.int16, device=dev)
         ops.conv2d(V(T(x16.reshape(-1), dev), 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2,
                    V(out, 8, cout + 16), scale=sc, shift=sh, act="relu", res1=V(T(r16.reshape(-1), dev), 0, cout),
-                   wt16=w16)
+                   res2=V(T(q16.reshape(-1), dev), 0, cout), wt16=w16)
     finally:
         ops.force_conv_config(None)
     want = ops.bf16_bits(ref.cpu().numpy()).view(np.int16).reshape(m, cout)
@@ -450,6 +452,14 @@ def test_pools_and_stem_bf16_rows(dev):
         got = out.cpu().numpy().reshape(-1, c + 8)
         assert np.array_equal(got[:, 8:], want), fn.__name__
         assert np.all(got[:, :8] == -1)
+    # nearest ×2 upsample of bf16 rows between channel slices (a copy: bit-exact)
+    up_in = T(x16.reshape(-1), dev)
+    up = torch.full((n * 4 * h * w * (c + 16),), -1, dtype=torch.int16, device=dev)
+    ops.upsample2x(V(up_in, 0, c), V(up, 8, c + 16), n, h, w, c)
+    u = up.cpu().numpy().reshape(n, 2 * h, 2 * w, c + 16)
+    src = x16.reshape(n, h, w, c)
+    assert np.array_equal(u[..., 8:8 + c], src.repeat(2, axis=1).repeat(2, axis=2))
+    assert np.all(u[..., :8] == -1) and np.all(u[..., 8 + c:] == -1)
     px = T(rng.uniform(0, 1, (2, 3, 37, 30)).astype(np.float32), dev)
     wt = T((rng.standard_normal((32, 27)) / 5).astype(np.float32), dev)
     sc, sh = T(rng.uniform(0.5, 1.5, 32).astype(np.float32), dev), T(rng.standard_normal(32).astype(np.float32), dev)
