@@ -132,6 +132,9 @@ typedef struct {
   int32_t B, S, Q, heads, head_dim, levels, points;
   int32_t level_h[4], level_w[4], level_start[4];
   float offset_scale;
+  /* ABI v10: value_bf16 (non-NULL) replaces value — the bf16 variant's value projection stored as bf16
+   * rows (same ld_value / value_col in elements); sampling and accumulation stay fp32. */
+  const uint16_t* value_bf16;
 } sp_msda_desc;
 
 int sp_abi_version(void);

@@ -57,6 +57,7 @@ class SpMsdaDesc(C.Structure):
         ("levels", i32), ("points", i32),
         ("level_h", i32 * 4), ("level_w", i32 * 4), ("level_start", i32 * 4),
         ("offset_scale", f32),
+        ("value_bf16", vp),
     ]
 
 

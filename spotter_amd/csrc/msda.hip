@@ -70,7 +70,17 @@ __global__ __launch_bounds__(256) void msda_kernel(const sp_msda_desc d) {
 // branching, so the 4·L·P loads of a lane are independent and stay in flight together. The grid is
 // remapped XCD-major: each XCD walks a contiguous run of queries (a few whole images), which keeps
 // an image's value rows in that XCD's L2 while its queries are being sampled.
-__global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, int lanes_per_q) {
+// VBF: the value rows are bf16 (value_bf16, the bf16 variant): each corner is one 8-byte load per lane.
+__device__ __forceinline__ float4 corner4(const float* v) { return *reinterpret_cast<const float4*>(v); }
+__device__ __forceinline__ float4 corner4(const uint16_t* v) {
+  const uint2 u = *reinterpret_cast<const uint2*>(v);
+  return make_float4(__builtin_bit_cast(float, u.x << 16), __builtin_bit_cast(float, u.x & 0xffff0000u),
+                     __builtin_bit_cast(float, u.y << 16), __builtin_bit_cast(float, u.y & 0xffff0000u));
+}
+
+template <typename VT>
+__global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, const VT* __restrict__ value,
+                                                       int lanes_per_q) {
   const int nwg = gridDim.x;
   const int orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -93,11 +103,11 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, int
   float den = 0.f;
   for (int i = 0; i < LP; ++i) den += expf(logit[i] - mx);
   const float nps = 1.0f / (float)d.points;
-  const float* vbase = d.value + (int64_t)b * d.S * d.ld_value + d.value_col + h * d.head_dim + c;
+  const VT* vbase = value + (int64_t)b * d.S * d.ld_value + d.value_col + h * d.head_dim + c;
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int l = 0; l < d.levels; ++l) {
     const int H = d.level_h[l], W = d.level_w[l];
-    const float* vl = vbase + (int64_t)d.level_start[l] * d.ld_value;
+    const VT* vl = vbase + (int64_t)d.level_start[l] * d.ld_value;
 #pragma unroll 4
     for (int p = 0; p < d.points; ++p) {
       const int i = l * d.points + p;
@@ -121,10 +131,10 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, int
       const bool vy0 = yi0 >= 0 && yi0 < H, vy1 = yi0 + 1 >= 0 && yi0 + 1 < H;
       const int cx0 = min(max(xi0, 0), W - 1), cx1 = min(max(xi0 + 1, 0), W - 1);
       const int cy0 = min(max(yi0, 0), H - 1), cy1 = min(max(yi0 + 1, 0), H - 1);
-      const float4 vnw = *reinterpret_cast<const float4*>(vl + ((int64_t)cy0 * W + cx0) * d.ld_value);
-      const float4 vne = *reinterpret_cast<const float4*>(vl + ((int64_t)cy0 * W + cx1) * d.ld_value);
-      const float4 vsw = *reinterpret_cast<const float4*>(vl + ((int64_t)cy1 * W + cx0) * d.ld_value);
-      const float4 vse = *reinterpret_cast<const float4*>(vl + ((int64_t)cy1 * W + cx1) * d.ld_value);
+      const float4 vnw = corner4(vl + ((int64_t)cy0 * W + cx0) * d.ld_value);
+      const float4 vne = corner4(vl + ((int64_t)cy0 * W + cx1) * d.ld_value);
+      const float4 vsw = corner4(vl + ((int64_t)cy1 * W + cx0) * d.ld_value);
+      const float4 vse = corner4(vl + ((int64_t)cy1 * W + cx1) * d.ld_value);
       // an invalid corner adds exactly +0 (same sum as skipping it, M2:79-81 zeros padding)
       wnw = (vy0 && vx0) ? wnw : 0.f;
       wne = (vy0 && vx1) ? wne : 0.f;
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, int
 
 extern "C" int sp_msda(const sp_msda_desc* d, void* stream) {
   using namespace sp;
-  SP_ARG_CHECK(d && d->value && d->off_aw && d->ref && d->out, "sp_msda: null args");
+  SP_ARG_CHECK(d && (d->value || d->value_bf16) && d->off_aw && d->ref && d->out, "sp_msda: null args");
   SP_ARG_CHECK(d->heads * d->head_dim <= 1024 && (d->heads * d->head_dim) % 64 == 0,
                "sp_msda: heads*head_dim must be a multiple of 64 <= 1024");
   SP_ARG_CHECK(d->levels >= 1 && d->levels <= 4 && d->points >= 1, "sp_msda: levels/points");
@@ -157,13 +167,19 @@ extern "C" int sp_msda(const sp_msda_desc* d, void* stream) {
   }
   SP_ARG_CHECK(total == d->S, "sp_msda: Σ H·W = %d != S = %d", total, d->S);
   const int C = d->heads * d->head_dim;
+  const bool vbf = d->value_bf16 != nullptr;
   const bool vec = d->head_dim % 4 == 0 && 256 % (C / 4) == 0 && d->ld_value % 4 == 0 && d->value_col % 4 == 0 &&
-                   d->ld_out % 4 == 0 && ((uintptr_t)d->value & 15) == 0 && ((uintptr_t)d->out & 15) == 0;
+                   d->ld_out % 4 == 0 && ((uintptr_t)(vbf ? (const void*)d->value_bf16 : (const void*)d->value) & (vbf ? 7 : 15)) == 0 &&
+                   ((uintptr_t)d->out & 15) == 0;
+  SP_ARG_CHECK(vec || !vbf, "sp_msda: bf16 value rows need head_dim %% 4 == 0, aligned rows, C / 4 dividing 256");
   const int64_t rows = (int64_t)d->B * d->Q;
   if (vec) {
     const int lanes = C / 4, qpw = 256 / lanes;
-    hipLaunchKernelGGL(msda_vec_kernel, dim3((unsigned)((rows + qpw - 1) / qpw)), dim3(256), 0, as_stream(stream),
-                       *d, lanes);
+    const dim3 grid((unsigned)((rows + qpw - 1) / qpw));
+    if (vbf)
+      hipLaunchKernelGGL(msda_vec_kernel<uint16_t>, grid, dim3(256), 0, as_stream(stream), *d, d->value_bf16, lanes);
+    else
+      hipLaunchKernelGGL(msda_vec_kernel<float>, grid, dim3(256), 0, as_stream(stream), *d, d->value, lanes);
   } else {
     hipLaunchKernelGGL(msda_kernel, dim3((unsigned)rows), dim3(C), 0, as_stream(stream), *d);
   }

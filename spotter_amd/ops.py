@@ -142,7 +142,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         last = out.off + (groups - 1) * group_stride + (rows_per_group - 1) * out.ld + cout
         if last > out.t.numel() or cout > out.ld:
             raise ValueError("conv.C grouped span exceeds output")
-        d.C = out.ptr
+        if out.is_bf16:
+            d.C_bf16 = out.ptr
+        else:
+            d.C = out.ptr
     elif out.is_bf16:  # bf16 output rows (RNE in the epilogue)
         d.C_bf16 = out.need(m, cout, "conv.C", bf16=True)
     else:
@@ -389,7 +392,10 @@ def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q
          shapes, starts, points, offset_scale):
     d = SpMsdaDesc()
     L = len(shapes)
-    d.value = value.need(B * S, value_col + heads * head_dim, "msda.value")
+    if value.is_bf16:  # the bf16 variant's value rows
+        d.value_bf16 = value.need(B * S, value_col + heads * head_dim, "msda.value", bf16=True)
+    else:
+        d.value = value.need(B * S, value_col + heads * head_dim, "msda.value")
     d.ld_value = value.ld
     d.value_col = value_col
     d.off_aw = off_aw.need(B * Q, heads * L * points * 3, "msda.off_aw")
@@ -406,7 +412,7 @@ def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q
     # larger than the 4 bilinear corners of every sample (1280²: 34.4 MB vs 14.7 MB per image), the
     # corner rows — plus offsets + weights + reference boxes per query and the output
     value_bytes = min(S, Q * L * points * 4) * heads * head_dim
-    nbytes = 4 * (B * value_bytes + B * Q * (heads * L * points * 3 + 4 + heads * head_dim))
+    nbytes = value.t.element_size() * B * value_bytes + 4 * B * Q * (heads * L * points * 3 + 4 + heads * head_dim)
     # per sample: 4 bilinear taps (multiply-add) + the attention weight
     flops = B * Q * heads * L * points * head_dim * 10
     _launch("msda", "sp_msda", (C.byref(d), stream()), flops, nbytes, (B, S, Q, heads, head_dim, L, points))

@@ -658,6 +658,31 @@ def test_attention(dev, n, heads, dh):
     np.testing.assert_allclose(out.cpu().numpy().reshape(B * n, D), ref, rtol=1e-4, atol=1e-5)
 
 
+def test_msda_bf16_value_rows(dev):
+    """sp_msda with bf16 value rows (value_bf16, ABI v10: the bf16 variant) against the fp32-row kernel on the
+    same bf16-representable values: the sampling arithmetic is fp32 either way, but the two instantiations
+    may contract the corner sums into fmas differently, so the bar is fp32 rounding (1e-6 of the scale)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(12)
+    B, Q, nH, dh, nL, nP = 2, 37, 8, 32, 3, 4
+    shapes, starts, S = [(16, 12), (8, 6), (4, 3)], [0, 192, 240], 252
+    D = nH * dh
+    v16, v32 = _bf16_rows(rng.standard_normal((B * S, 2 * D)).astype(np.float32))
+    offaw = np.concatenate([rng.standard_normal((B * Q, nH * nL * nP * 2)) * 2.0,
+                            rng.standard_normal((B * Q, nH * nL * nP))], 1).astype(np.float32)
+    ref = np.concatenate([rng.uniform(0.05, 0.95, (B * Q, 2)), rng.uniform(0.05, 0.6, (B * Q, 2))], 1).astype(np.float32)
+    outs = []
+    for vals in (v32, v16):
+        out = torch.empty(B * Q * D, device=dev)
+        ops.msda(V(T(vals.reshape(-1), dev), 0, 2 * D), D, V(T(offaw.reshape(-1), dev), 0, offaw.shape[1]),
+                 T(ref, dev), V(out, 0, D), B, S, Q, nH, dh, shapes, starts, nP, 0.5)
+        outs.append(out.cpu().numpy())
+    d = np.abs(outs[0] - outs[1]).max()
+    assert d <= 1e-6 * np.abs(outs[0]).max(), d
+
+
 @pytest.mark.parametrize("pad", [0, 1])
 def test_msda_matches_oracle(dev, pad):
     """MSDA core incl. out-of-range sampling points (zero padding) vs oracle.grid_sample_bilinear.
