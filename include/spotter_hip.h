@@ -198,6 +198,11 @@ int sp_stem_conv3x3s2_nchw(const float* x, const float* wt, const float* scale, 
 /* The same with bf16 output rows (ABI v10: the bf16 variant; fp32 arithmetic, RNE at the store). */
 int sp_stem_conv3x3s2_nchw_bf16(const float* x, const float* wt, const float* scale, const float* shift, uint16_t* y,
                                 int n, int h, int w, int cout, int act, void* stream);
+/* Stem convs 2 and 3 of the bf16 variant (ABI v10): 3x3 stride 1 pad 1, Cin 32 → Cout 32 or 64, dense NHWC
+ * bf16 rows in and out, weights w16 bf16 [Cout][3][3][32], FrozenBN (scale, shift) + act (0 none, 1 relu)
+ * in fp32, RNE at the store. Direct LDS-halo convolution (RN:78-103). */
+int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const float* scale, const float* shift, uint16_t* y,
+                        int n, int h, int w, int cout, int act, void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
  * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
 int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);

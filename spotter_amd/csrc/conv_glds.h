@@ -337,10 +337,90 @@ __device__ __forceinline__ void glds_zero(f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M
   }
 }
 
+// Residual epilogue with the res1 tile fetched by LDS-DMA (variant 2, `EPV`): the plain epilogue fetches
+// res1 as float4 loads four tasks at a time, a latency chain that the short-K residual GEMMs (the
+// bottleneck expands) spend most of their epilogue in. Here each wave DMAs its whole residual band (32
+// rows × 32·TN columns, row-major, lane-linear 16-byte pieces: no VGPRs) into its own LDS slab, combines
+// it with the accumulators in the MFMA layout (BN affine, + res1, act: epilogue_vec's order, so the
+// result is bit-identical), writes the sums back into the slab and stores row-major float4s. Used for
+// fp32 res1 without row_scale; res2 is added in the store pass.
+template <int TM, int TN, int NB, bool L16>
+__device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
+                                                 int nb, int lane) {
+  constexpr int WN = TN * 32;
+  constexpr int C4 = WN / 4;               // float4 columns per slab row
+  constexpr int NI = NB * 32 * C4 / 64;    // 1 KB DMA pieces (and float4 store tasks) per lane per round
+  constexpr int NCOL = L16 ? 2 : 1;        // distinct accumulator columns of a lane per 32-wide block
+  const sp_conv_desc& d = p.d;
+  const int r = lane & 31, h = lane >> 5;
+  float scv[TN][NCOL], shv[TN][NCOL];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      const int n = nb + j * 32 + (L16 ? 16 * k + (lane & 15) : r);
+      const bool ok = n < d.Cout;
+      scv[j][k] = ok && d.scale ? d.scale[n] : 1.0f;
+      shv[j][k] = ok && d.shift ? d.shift[n] : 0.0f;
+    }
+  const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)region);
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+#pragma unroll
+  for (int i0 = 0; i0 < TM; i0 += NB) {
+    const int64_t mr = mb + i0 * 32;
+    if (i0) __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int u = 0; u < NI; ++u) {  // not unrolled: the accumulators are live, keep the addresses out of VGPRs
+      const int idx = u * 64 + lane;
+      const int row = idx / C4;
+      const int n = nb + (idx - row * C4) * 4;
+      const int64_t m = mr + row;
+      const void* src = (m < p.M && n < d.Cout) ? static_cast<const void*>(d.res1 + m * d.ldr1 + n)
+                                                 : static_cast<const void*>(zero);
+      glds16(src, rbase + u * 1024);
+    }
+    wait_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          const int k = L16 ? (q >> 2) & 1 : 0;
+          float* slot = region + (i * 32 + rr) * WN + j * 32 + cc;
+          float v = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
+          v += *slot;
+          *slot = act_apply(v, d.act);
+          // one element at a time: hoisting the slab reads would hold a second accumulator's worth of VGPRs
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int t = 0; t < NI; ++t) {
+      const int cidx = lane + 64 * t;
+      const int row = cidx / C4;
+      const int col = (cidx - row * C4) * 4;
+      const int64_t m = mr + row;
+      const int n = nb + col;
+      if (m >= p.M || n >= d.Cout) continue;
+      float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
+      if (d.res2) {
+        const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
+        v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      }
+      store_out4(d, m, n, v);
+    }
+  }
+}
+
 // Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
 // Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
 // index within that member.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int APL>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int APL, int EPV = 1>
 __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, int wg, f32x16 (&acc)[TM][TN],
                                               f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;  // the kernel's own LDS size decides the band count
@@ -362,13 +442,19 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
 #pragma unroll
         for (int q = 0; q < 16; ++q) acc[i][j][q] = acc4[2 * i + (q >> 3)][2 * j + ((q >> 2) & 1)][q & 3];
   }
-  epilogue_tile<TM, TN, C::NB, M16>(p, smemf + wave * (C::NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
-                                    n0 + wn * TN * 32, lane);
+  float* region = smemf + wave * (C::NB * 32 * TN * 32);
+  // EPV 2 kernels carry only the residual-DMA epilogue (launch_glds checks its conditions on the host): a
+  // runtime choice between the two made hipcc read all accumulators out of the AGPRs ahead of the branch
+  if constexpr (EPV == 2)
+    epilogue_tile_rd<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
+  else
+    epilogue_tile<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 }
 
 // OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained). Applied to the
 // 1×1 fast-path instantiations only (launch_glds): the general path's extra address registers spill.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1, int APL = 0>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int OCC = 1, int APL = 0,
+          int EPV = 1>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const ConvArgs p) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;
   __shared__ uint4 smem[C::SMEM];
@@ -388,7 +474,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
   ConvArgs q = p;
   q.d.C += (int64_t)bi * p.bs_c;
-  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16, APL>(q, smem, wg, acc, acc4);
+  glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16, APL, EPV>(q, smem, wg, acc, acc4);
 #if SP_GLDS_STAMP
   __syncthreads();
   GLDS_STAMP(3);
@@ -412,7 +498,7 @@ inline bool t1_ok(const ConvArgs& a) {
 
 // AB: the bf16-A-plane variants (ConvArgs::A16) are compiled for this tile.
 template <int WM, int WN, int TM, int TN, int NS, int BK = 32, bool M16 = false, int OCC = 1, bool AB = false>
-int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
+int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   if (a.d.Cin % BK || a.K % BK) {
     set_error("sp_conv2d: LDS-DMA kernel needs Cin %% %d == 0 (Cin=%d)", BK, a.d.Cin);
     return -1;
@@ -444,8 +530,13 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
   // the 1×1 fast path where it applies, else the general implicit GEMM
   const bool t1 = t1_ok(a);
   const dim3 blk(64 * WM * WN);
+  // the residual-DMA epilogue: fp32 res1, float4 epilogue, no split-K / row_scale / bf16 rows
+  if (epv == 2 && !(a.vec_epi && a.splits == 1 && a.d.res1 && !a.d.row_scale && !a.d.C_bf16 && !a.d.res2_bf16))
+    epv = 1;
   if constexpr (fit3) {
-    if (planes == 3 && !a16 && t1)
+    if (planes == 3 && !a16 && t1 && epv == 2)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 2>), grid, blk, 0, s, ab);
+    else if (planes == 3 && !a16 && t1)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC>), grid, blk, 0, s, ab);
     else if (planes == 3 && !a16)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1>), grid, blk, 0, s, ab);
@@ -519,12 +610,12 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s) {
 constexpr int kGldsParts = 6;
 
 template <int PART>
-int glds_part(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+int glds_part(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
   switch (cfg) {
 #define SP_GLDS_CASE(id, WM, WN, TM, TN, NS, BK, M16, OCC, AB)                          \
   case id:                                                                            \
     if constexpr ((id) % kGldsParts == PART)                                          \
-      return launch_glds<WM, WN, TM, TN, NS, BK, M16, OCC, AB>(a, planes, s);        \
+      return launch_glds<WM, WN, TM, TN, NS, BK, M16, OCC, AB>(a, planes, s, epv);        \
     else                                                                              \
       return -2;
     SP_GLDS_CONFIGS(SP_GLDS_CASE)

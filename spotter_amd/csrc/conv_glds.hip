@@ -8,43 +8,46 @@ namespace sp {
 
 #if SP_GLDS_STAMP
 namespace {
-int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
   switch (k) {
-    case 0: return glds_part<0>(a, planes, cfg, s);
-    case 1: return glds_part<1>(a, planes, cfg, s);
-    case 2: return glds_part<2>(a, planes, cfg, s);
-    case 3: return glds_part<3>(a, planes, cfg, s);
-    case 4: return glds_part<4>(a, planes, cfg, s);
-    default: return glds_part<5>(a, planes, cfg, s);
+    case 0: return glds_part<0>(a, planes, cfg, s, epv);
+    case 1: return glds_part<1>(a, planes, cfg, s, epv);
+    case 2: return glds_part<2>(a, planes, cfg, s, epv);
+    case 3: return glds_part<3>(a, planes, cfg, s, epv);
+    case 4: return glds_part<4>(a, planes, cfg, s, epv);
+    default: return glds_part<5>(a, planes, cfg, s, epv);
   }
 }
 }  // namespace
 #else
-int launch_glds_part0(const ConvArgs& a, int planes, int cfg, hipStream_t s);
-int launch_glds_part1(const ConvArgs& a, int planes, int cfg, hipStream_t s);
-int launch_glds_part2(const ConvArgs& a, int planes, int cfg, hipStream_t s);
-int launch_glds_part3(const ConvArgs& a, int planes, int cfg, hipStream_t s);
-int launch_glds_part4(const ConvArgs& a, int planes, int cfg, hipStream_t s);
-int launch_glds_part5(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+int launch_glds_part0(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
+int launch_glds_part1(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
+int launch_glds_part2(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
+int launch_glds_part3(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
+int launch_glds_part4(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
+int launch_glds_part5(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv);
 namespace {
-int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
   switch (k) {
-    case 0: return launch_glds_part0(a, planes, cfg, s);
-    case 1: return launch_glds_part1(a, planes, cfg, s);
-    case 2: return launch_glds_part2(a, planes, cfg, s);
-    case 3: return launch_glds_part3(a, planes, cfg, s);
-    case 4: return launch_glds_part4(a, planes, cfg, s);
-    default: return launch_glds_part5(a, planes, cfg, s);
+    case 0: return launch_glds_part0(a, planes, cfg, s, epv);
+    case 1: return launch_glds_part1(a, planes, cfg, s, epv);
+    case 2: return launch_glds_part2(a, planes, cfg, s, epv);
+    case 3: return launch_glds_part3(a, planes, cfg, s, epv);
+    case 4: return launch_glds_part4(a, planes, cfg, s, epv);
+    default: return launch_glds_part5(a, planes, cfg, s, epv);
   }
 }
 }  // namespace
 #endif
 static_assert(kGldsParts == 6, "one conv_glds_p<k>.hip per part");
 
-// The LDS-DMA configurations (see launch_mfma16); -2 when cfg is not one of them.
+// The LDS-DMA configurations (see launch_mfma16); -2 when cfg is not one of them. cfg + 100: the same tile
+// with the LDS-DMA residual epilogue (epilogue_tile_rd) on the split mode's 1×1 path.
 int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
+  const int epv = cfg >= 100 ? 2 : 1;
+  if (cfg >= 100) cfg -= 100;
   if (a.d.A2 || cfg < 11 || cfg > 65) return -2;
-  return glds_part_k(cfg % kGldsParts, a, planes, cfg, s);
+  return glds_part_k(cfg % kGldsParts, a, planes, cfg, s, epv);
 }
 
 }  // namespace sp

@@ -4,8 +4,8 @@
 
 #if !SP_GLDS_STAMP
 namespace sp {
-int launch_glds_part3(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
-  return glds_part<3>(a, planes, cfg, s);
+int launch_glds_part3(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
+  return glds_part<3>(a, planes, cfg, s, epv);
 }
 }  // namespace sp
 #endif

@@ -1418,11 +1418,20 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  if (((cfg >= 11 && cfg <= 20) || (cfg >= 33 && cfg <= 38) || (cfg >= 41 && cfg <= 51) || (cfg >= 62 && cfg <= 65)) && !a.d.A2) {
+  // The LDS-DMA residual epilogue (conv_glds.h epilogue_tile_rd, "cfg + 100") on the split mode's residual
+  // launches, for the tiles where it measured faster: 1.02-1.28x on the bottleneck expands (46, 45, 47, 14, 12,
+  // 63), 0.59-0.96x on the 256-wide-N / TN = 4 four-wave tiles (33, 44), bit-identical either way
+  // (profiles/r3/x3/ab_residual_dma_epilogue.jsonl)
+  if (planes == 3 && !a.A16 && a.d.res1 && !a.d.row_scale && a.vec_epi && a.splits == 1 && !a.d.C_bf16 &&
+      (cfg == 11 || cfg == 12 || cfg == 13 || cfg == 14 || cfg == 16 || cfg == 41 || cfg == 43 || cfg == 45 ||
+       cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64 || cfg == 65))
+    cfg += 100;
+  const int gc = cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;  // cfg + 100: the LDS-DMA residual epilogue variant
+  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || cfg > 75 || (cfg >= 73 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

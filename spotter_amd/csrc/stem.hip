@@ -134,3 +134,151 @@ extern "C" int sp_stem_conv3x3s2_nchw_bf16(const float* x, const float* wt, cons
                                            uint16_t* y, int n, int h, int w, int cout, int act, void* stream) {
   return stem_launch("sp_stem_conv3x3s2_nchw_bf16", x, wt, scale, shift, y, n, h, w, cout, act, stream);
 }
+
+// ---------------------------------------------------------------------------------------------
+// Stem convs 2 and 3 of the bf16 variant (RN:78-103: 3×3 stride 1 pad 1, Cin 32 → Cout 32 / 64, FrozenBN,
+// ReLU) as a direct LDS-halo convolution on bf16 rows (ABI v10). As an implicit GEMM these ran at
+// 179 / 361 TF (C3, 26.2 M output rows): K = 288 gives a 64-wide tile little reuse, a 32-wide Cout
+// wastes half of it, and every A row is fetched once per tap. Here a workgroup stages its input halo —
+// (4·RPW + 2) rows × (64 + 2) pixels × 32 channels, bf16 — and all 9·Cout·32 weights in LDS once, then
+// each wave computes RPW output rows × 64 pixels × Cout on v_mfma_f32_32x32x16_bf16 with the roles
+// transposed (A = weights [Cout × k], B = pixels [k × 64]): the accumulator of lane (pixel r, half h)
+// then holds four runs of 4 consecutive channels of one pixel, stored as 8-byte bf16 quads after the
+// BN affine + act (fp32). LDS chunks are swizzled (chunk ^ ((row >> 2) & 3)) so a 16-lane group's
+// 16-byte reads of 16 consecutive pixels / channels cover all 64 banks.
+namespace sp {
+namespace {
+
+typedef __bf16 bf16x8_s __attribute__((ext_vector_type(8)));
+typedef float f32x16_s __attribute__((ext_vector_type(16)));
+
+constexpr int C3_TW = 64;  // output pixels per wave row
+
+template <int CO, int RPW>
+__global__ __launch_bounds__(256, 2) void conv3x3_c32_bf16_kernel(const uint16_t* __restrict__ x,
+                                                                  const uint16_t* __restrict__ w16,
+                                                                  const float* __restrict__ scale,
+                                                                  const float* __restrict__ shift,
+                                                                  uint16_t* __restrict__ y, int nimg, int h, int w,
+                                                                  int tiles_x, int tiles_y, int act) {
+  constexpr int TH = 4 * RPW, HR = TH + 2, HC = C3_TW + 2;
+  constexpr int HALO = HR * HC * 4;  // 16-byte chunks
+  constexpr int WCH = 9 * CO * 4;    // 16-byte chunks of the weights
+  constexpr int TMN = CO / 32;       // 32-channel blocks
+  __shared__ uint4 lds[HALO + WCH];
+  uint4* halo = lds;
+  uint4* wl = lds + HALO;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // weights: global [CO][9 taps][32 ci] bf16 (the packed [Cout][K] form) → LDS [tap][n][chunk ^ swz(n)], once
+  // per workgroup: the grid is persistent (a few workgroups per CU walk the tiles), since per 256-pixel
+  // tile the weights are as many bytes as the input halo
+  for (int i = tid; i < WCH; i += 256) {
+    const int c = i & 3, tn = i >> 2, n = tn / 9, tap = tn - n * 9;
+    wl[(tap * CO + n) * 4 + (c ^ ((n >> 2) & 3))] = *reinterpret_cast<const uint4*>(w16 + (int64_t)i * 8);
+  }
+  const int64_t ntiles = (int64_t)nimg * tiles_x * tiles_y;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int64_t t = tile;
+  const int tx = (int)(t % tiles_x);
+  t /= tiles_x;
+  const int ty = (int)(t % tiles_y);
+  const int b = (int)(t / tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * C3_TW;
+  __syncthreads();  // the previous tile's halo reads are done
+  // input halo: rows oy0-1 .. oy0+TH, pixels ox0-1 .. ox0+64 (zero outside the map)
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < HALO; i += 256) {
+    const int c = i & 3, rc = i >> 2, r = rc / HC, col = rc - r * HC;
+    const int iy = oy0 - 1 + r, ix = ox0 - 1 + col;
+    const bool ok = (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+    halo[rc * 4 + (c ^ ((col >> 2) & 3))] =
+        ok ? *reinterpret_cast<const uint4*>(x + (((int64_t)b * h + iy) * w + ix) * 32 + c * 8) : z;
+  }
+  __syncthreads();
+
+  const int r = lane & 31, hh = lane >> 5;
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int orow = wave * RPW + rr;  // output row within the tile
+    f32x16_s acc[TMN][2];
+#pragma unroll
+    for (int i = 0; i < TMN; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int ch = 2 * s + hh;  // k chunk: ci 16s + 8hh .. +7
+          bf16x8_s fa[TMN], fb[2];
+#pragma unroll
+          for (int i = 0; i < TMN; ++i) {
+            const int n = i * 32 + r;
+            fa[i] = *reinterpret_cast<const bf16x8_s*>(wl + (tap * CO + n) * 4 + (ch ^ ((n >> 2) & 3)));
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int col = j * 32 + r + kw;
+            fb[j] = *reinterpret_cast<const bf16x8_s*>(halo + ((orow + kh) * HC + col) * 4 + (ch ^ ((col >> 2) & 3)));
+          }
+#pragma unroll
+          for (int i = 0; i < TMN; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    // epilogue: lane (pixel r of block j, half hh) holds channels i·32 + 8g + 4hh .. +3 in acc[i][j][4g .. 4g+3]
+    const int oy = oy0 + orow;
+    if (oy < h) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ox = ox0 + j * 32 + r;
+        if (ox >= w) continue;
+        uint16_t* yrow = y + (((int64_t)b * h + oy) * w + ox) * CO;
+#pragma unroll
+        for (int i = 0; i < TMN; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n0 = i * 32 + 8 * g + 4 * hh;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float u = fmaf(acc[i][j][4 * g + e], scale[n0 + e], shift[n0 + e]);
+              v[e] = act ? fmaxf(u, 0.f) : u;
+            }
+            *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+          }
+      }
+    }
+  }
+  }  // tiles
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const float* scale, const float* shift,
+                                   uint16_t* y, int n, int h, int w, int cout, int act, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(x && w16 && scale && shift && y && n > 0 && h > 0 && w > 0 && (cout == 32 || cout == 64) &&
+                   (act == 0 || act == 1) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w16 & 15) == 0 &&
+                   ((uintptr_t)y & 7) == 0,
+               "sp_conv3x3_c32_bf16: bad args (Cin 32, Cout 32 or 64, act none/relu, aligned dense bf16 rows)");
+  constexpr int RPW = 1;
+  const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + 4 * RPW - 1) / (4 * RPW);
+  const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
+  // persistent grid: as many workgroups as fit on the chip at once (2 per CU at Cout 64, 3 at Cout 32)
+  const int64_t cap = (int64_t)g_num_cus * (cout == 32 ? 3 : 2);
+  const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+  if (cout == 32)
+    hipLaunchKernelGGL((conv3x3_c32_bf16_kernel<32, RPW>), dim3(grid), dim3(256), 0, as_stream(stream), x,
+                       w16, scale, shift, y, n, h, w, tiles_x, tiles_y, act);
+  else
+    hipLaunchKernelGGL((conv3x3_c32_bf16_kernel<64, RPW>), dim3(grid), dim3(256), 0, as_stream(stream), x,
+                       w16, scale, shift, y, n, h, w, tiles_x, tiles_y, act);
+  return check_launch("sp_conv3x3_c32_bf16");
+}

@@ -503,8 +503,14 @@ class Engine:
             px = self._buf("px_nhwc", B, H, W, 3)
             ops.nchw_to_nhwc(pixel_values, px)
             self._cv(view(px, 3), B, H, W, c0, 2, view(s0, e // 2), act=self.act_bb)
-        self._cv(view(s0, e // 2), B, h1, w1, self.stem[1], 1, view(s1, e // 2), act=self.act_bb)
-        self._cv(view(s1, e // 2), B, h1, w1, self.stem[2], 1, view(s2, e), act=self.act_bb)
+        for src, cw, dst in ((s0, self.stem[1], s1), (s1, self.stem[2], s2)):
+            if self.bf16_store and cw.cin == 32 and cw.k == 3 and cw.cout in (32, 64) and self.act_bb in ("relu", None):
+                # the bf16 variant's Cin-32 stem 3×3s: direct LDS-halo kernel (the implicit GEMM re-fetched every
+                # A row per tap and wasted half a 64-wide tile on Cout 32)
+                ops.conv3x3_c32_bf16(view(src, cw.cin), cw.w16, cw.scale, cw.shift, view(dst, cw.cout), B, h1, w1,
+                                     cw.cout, act=self.act_bb)
+            else:
+                self._cv(view(src, cw.cin), B, h1, w1, cw, 1, view(dst, cw.cout), act=self.act_bb)
         h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1
         b0 = self.blocks[0]
         if "fused" in b0 and b0["sc"] == "conv":

@@ -325,6 +325,22 @@ def stem_conv_nchw(x: torch.Tensor, wt: torch.Tensor, scale: torch.Tensor, shift
     return ho, wo
 
 
+def conv3x3_c32_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int,
+                     w: int, cout: int, act=None):
+    """Stem convs 2 / 3 of the bf16 variant (RN:78-103: 3×3/1, Cin 32 → Cout 32 or 64, FrozenBN, ReLU) on dense
+    bf16 NHWC rows: the direct LDS-halo kernel sp_conv3x3_c32_bf16."""
+    if not (x.is_bf16 and y.is_bf16) or x.ld != 32 or y.ld != cout:
+        raise ValueError("conv3x3_c32_bf16: dense bf16 rows (ld 32 in, Cout out) expected")
+    if w16.dtype != torch.int16 or w16.numel() != cout * 288 or scale.numel() < cout or shift.numel() < cout:
+        raise ValueError("conv3x3_c32_bf16: weight / affine size mismatch")
+    m = n * h * w
+    xp = x.need(m, 32, "c32.x", bf16=True)
+    yp = y.need(m, cout, "c32.y", bf16=True)
+    _launch("conv", "sp_conv3x3_c32_bf16", (xp, w16.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, n, h, w,
+                                            cout, ACT[act], stream()),
+            2 * m * cout * 288, 2 * (m * 32 + cout * 288 + m * cout), (m, cout, 288, 3, 1, "bf16-direct"))
+
+
 def _pool_out(y, m: int, c: int, what: str):
     """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
     if isinstance(y, V):

@@ -433,6 +433,33 @@ def test_conv2d_bf16_rows_in_and_out(dev, k, stride, cfg):
     assert np.all(got[:, :8] == -1) and np.all(got[:, 8 + cout:] == -1)
 
 
+@pytest.mark.parametrize("cout,act,hw", [(32, "relu", (13, 70)), (64, "relu", (9, 129)), (64, None, (4, 64)),
+                                         (32, None, (1, 1))])
+def test_conv3x3_c32_bf16_direct(dev, cout, act, hw):
+    """sp_conv3x3_c32_bf16 (the bf16 variant's direct stem 3×3, ABI v10) equals the implicit-GEMM bf16 path on
+    the same bf16 rows bit for bit: both sum the 288-deep k in (tap, 16-channel) order with the same
+    v_mfma_f32_32x32x16_bf16 blocks. Ragged tile edges in both directions, one-pixel maps."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(51 + cout)
+    n, (h, w) = 2, hw
+    m = n * h * w
+    x16, _ = _bf16_rows(rng.standard_normal((m, 32)).astype(np.float32))
+    wt = (rng.standard_normal((cout, 288)) / 17).astype(np.float32)
+    w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
+    sc, sh = T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev), T(rng.standard_normal(cout).astype(np.float32), dev)
+    xd = T(x16.reshape(-1), dev)
+    ref = torch.full((m * cout,), -1, dtype=torch.int16, device=dev)
+    ops.force_conv_config("14")
+    ops.conv2d(V(xd, 0, 32), n, h, w, 32, T(wt, dev), cout, 3, 1, 1, V(ref, 0, cout), scale=sc, shift=sh, act=act,
+               wt16=w16)
+    ops.force_conv_config(None)
+    out = torch.full((m * cout,), -1, dtype=torch.int16, device=dev)
+    ops.conv3x3_c32_bf16(V(xd, 0, 32), w16, sc, sh, V(out, 0, cout), n, h, w, cout, act=act)
+    assert np.array_equal(out.cpu().numpy(), ref.cpu().numpy())
+
+
 def test_pools_and_stem_bf16_rows(dev):
     """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32
     kernels on the same bf16-representable inputs with the result rounded to bf16 (max: exact)."""

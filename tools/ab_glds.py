@@ -35,6 +35,9 @@ SHAPES = [
     (32, 40, 40, 256, 256, "wino"),
     (32, 40, 40, 384, 384, "wino"),
     (32, 20, 20, 512, 512, "wino"),
+    (32, 80, 80, 128, 512, True, "relu"),     # stage-1 expand (3 / step)
+    (32, 160, 160, 64, 256, True, "relu"),    # stage-0 expand (2 / step)
+    (32, 20, 20, 512, 2048, True, "relu"),    # stage-4 expand (2 / step)
 ]
 EDGES = [(1, 1, 1000, 256, 192, True, "relu"), (3, 7, 9, 128, 320, False, None), (1, 1, 77, 512, 128, True, None)]
 
