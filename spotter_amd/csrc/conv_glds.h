@@ -342,8 +342,9 @@ __device__ __forceinline__ void glds_zero(f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M
 // bottleneck expands) spend most of their epilogue in. Here each wave DMAs its whole residual band (32
 // rows × 32·TN columns, row-major, lane-linear 16-byte pieces: no VGPRs) into its own LDS slab, combines
 // it with the accumulators in the MFMA layout (BN affine, + res1, act: epilogue_vec's order, so the
-// result is bit-identical), writes the sums back into the slab and stores row-major float4s. Used for
-// fp32 res1 without row_scale; res2 is added in the store pass.
+// result is bit-identical), writes the sums back into the slab and stores row-major float4s. Without a
+// residual the same combine still saves the per-task BN scale / shift loads (one pair per lane and column
+// block instead). Used for fp32 res1 (or none) without row_scale; res2 is added in the store pass.
 template <int TM, int TN, int NB, bool L16>
 __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
                                                  int nb, int lane) {
@@ -366,12 +367,13 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
   const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)region);
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+  const bool res = d.res1 != nullptr;  // without a residual: the same combine, BN constants hoisted per lane
 #pragma unroll
   for (int i0 = 0; i0 < TM; i0 += NB) {
     const int64_t mr = mb + i0 * 32;
     if (i0) __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
-    for (int u = 0; u < NI; ++u) {  // not unrolled: the accumulators are live, keep the addresses out of VGPRs
+    for (int u = 0; u < (res ? NI : 0); ++u) {  // not unrolled: the accumulators are live, keep addresses out of VGPRs
       const int idx = u * 64 + lane;
       const int row = idx / C4;
       const int n = nb + (idx - row * C4) * 4;
@@ -380,7 +382,7 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
                                                  : static_cast<const void*>(zero);
       glds16(src, rbase + u * 1024);
     }
-    wait_vmcnt<0>();
+    if (res) wait_vmcnt<0>();
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
@@ -392,7 +394,7 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
           const int k = L16 ? (q >> 2) & 1 : 0;
           float* slot = region + (i * 32 + rr) * WN + j * 32 + cc;
           float v = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
-          v += *slot;
+          if (res) v += *slot;
           *slot = act_apply(v, d.act);
           // one element at a time: hoisting the slab reads would hold a second accumulator's worth of VGPRs
           __builtin_amdgcn_sched_barrier(0);
@@ -530,8 +532,8 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   // the 1×1 fast path where it applies, else the general implicit GEMM
   const bool t1 = t1_ok(a);
   const dim3 blk(64 * WM * WN);
-  // the residual-DMA epilogue: fp32 res1, float4 epilogue, no split-K / row_scale / bf16 rows
-  if (epv == 2 && !(a.vec_epi && a.splits == 1 && a.d.res1 && !a.d.row_scale && !a.d.C_bf16 && !a.d.res2_bf16))
+  // the residual-DMA epilogue: float4 epilogue, no split-K / row_scale / bf16 rows (res1 fp32 or none)
+  if (epv == 2 && !(a.vec_epi && a.splits == 1 && !a.d.row_scale && !a.d.C_bf16 && !a.d.res1_bf16 && !a.d.res2_bf16))
     epv = 1;
   if constexpr (fit3) {
     if (planes == 3 && !a16 && t1 && epv == 2)
