@@ -419,6 +419,80 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
   }
 }
 
+// The same slab epilogue for bf16 rows (variant 3: the bf16 variant, C_bf16 out, res1_bf16 or no residual, no
+// res2): the wave's slab (4 bytes per accumulator) holds the residual band as bf16 in its first half (LDS-DMA,
+// 16-byte pieces of 8 channels) and the rounded outputs in its second half; the store pass writes 8-byte
+// quads. Same arithmetic and rounding as epilogue_vec + store_out4: bit-identical.
+template <int TM, int TN, int NB, bool L16>
+__device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
+                                                   int nb, int lane) {
+  constexpr int WN = TN * 32;
+  constexpr int NI = NB * 32 * WN / 8 / 64;  // 16-byte residual pieces per lane per round
+  constexpr int NQ = NB * 32 * WN / 4 / 64;  // 8-byte output quads per lane per round
+  constexpr int NCOL = L16 ? 2 : 1;
+  static_assert(NI * 64 * 8 == NB * 32 * WN && NQ * 64 * 4 == NB * 32 * WN, "slab pieces");
+  const sp_conv_desc& d = p.d;
+  const int r = lane & 31, h = lane >> 5;
+  float scv[TN][NCOL], shv[TN][NCOL];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      const int n = nb + j * 32 + (L16 ? 16 * k + (lane & 15) : r);
+      const bool ok = n < d.Cout;
+      scv[j][k] = ok && d.scale ? d.scale[n] : 1.0f;
+      shv[j][k] = ok && d.shift ? d.shift[n] : 0.0f;
+    }
+  uint16_t* res16 = reinterpret_cast<uint16_t*>(region);
+  uint16_t* out16 = res16 + NB * 32 * WN;
+  const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)region);
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+  const bool res = d.res1_bf16 != nullptr;
+#pragma unroll
+  for (int i0 = 0; i0 < TM; i0 += NB) {
+    const int64_t mr = mb + i0 * 32;
+    if (i0) __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int u = 0; u < (res ? NI : 0); ++u) {
+      const int idx = u * 64 + lane;
+      const int row = idx / (WN / 8);
+      const int n = nb + (idx - row * (WN / 8)) * 8;
+      const int64_t m = mr + row;
+      const void* src = (m < p.M && n < d.Cout) ? static_cast<const void*>(d.res1_bf16 + m * d.ldr1 + n)
+                                                 : static_cast<const void*>(zero);
+      glds16(src, rbase + u * 1024);
+    }
+    if (res) wait_vmcnt<0>();
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          const int k = L16 ? (q >> 2) & 1 : 0;
+          const int pos = (i * 32 + rr) * WN + j * 32 + cc;
+          float v = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
+          if (res) v += bf16_lo(res16[pos]);
+          out16[pos] = (uint16_t)(pack_bf16x2(act_apply(v, d.act), 0.f) & 0xffffu);
+        }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+    for (int t = 0; t < NQ; ++t) {
+      const int cidx = lane + 64 * t;
+      const int row = cidx / (WN / 4);
+      const int col = (cidx - row * (WN / 4)) * 4;
+      const int64_t m = mr + row;
+      const int n = nb + col;
+      if (m >= p.M || n >= d.Cout) continue;
+      *reinterpret_cast<uint2*>(d.C_bf16 + out_off(d, m) + n) = *reinterpret_cast<const uint2*>(out16 + row * WN + col);
+    }
+  }
+}
+
 // Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
 // Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
 // index within that member.
@@ -449,6 +523,8 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
   // runtime choice between the two made hipcc read all accumulators out of the AGPRs ahead of the branch
   if constexpr (EPV == 2)
     epilogue_tile_rd<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
+  else if constexpr (EPV == 3)
+    epilogue_tile_rd16<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
   else
     epilogue_tile<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 }
@@ -532,9 +608,16 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   // the 1×1 fast path where it applies, else the general implicit GEMM
   const bool t1 = t1_ok(a);
   const dim3 blk(64 * WM * WN);
-  // the residual-DMA epilogue: float4 epilogue, no split-K / row_scale / bf16 rows (res1 fp32 or none)
-  if (epv == 2 && !(a.vec_epi && a.splits == 1 && !a.d.row_scale && !a.d.C_bf16 && !a.d.res1_bf16 && !a.d.res2_bf16))
-    epv = 1;
+  // the slab epilogues: fp32 rows (2: res1 fp32 or none) or bf16 rows (3: C_bf16, res1_bf16 or none, no res2);
+  // float4 epilogue, no split-K / row_scale
+  if (epv >= 2) {
+    const sp_conv_desc& d = a.d;
+    const bool base = a.vec_epi && a.splits == 1 && !d.row_scale;
+    const bool f32ok = base && !d.C_bf16 && !d.res1_bf16 && !d.res2_bf16;
+    const bool bf16ok = base && d.C_bf16 && !d.res1 && !d.res2 && !d.res2_bf16 &&
+                        (!d.res1_bf16 || ((reinterpret_cast<uintptr_t>(d.res1_bf16) & 15) == 0 && d.ldr1 % 8 == 0));
+    epv = f32ok ? 2 : bf16ok ? 3 : 1;
+  }
   if constexpr (fit3) {
     if (planes == 3 && !a16 && t1 && epv == 2)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 2>), grid, blk, 0, s, ab);
@@ -556,8 +639,12 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1, 1, 3>), grid, blk, 0, s, ab);
   }
   if constexpr (fit1a) {
-    if (planes != 3 && a16 && t1)
+    if (planes != 3 && a16 && t1 && epv == 3)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC, 1, 3>), grid, blk, 0, s, ab);
+    else if (planes != 3 && a16 && t1)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC, 1>), grid, blk, 0, s, ab);
+    else if (planes != 3 && a16 && epv == 3)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1, 1, 1, 3>), grid, blk, 0, s, ab);
     else if (planes != 3 && a16)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1, 1, 1>), grid, blk, 0, s, ab);
   }

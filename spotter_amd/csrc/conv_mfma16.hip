@@ -1357,8 +1357,12 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
 // 14 = 64×64 3 stages, 15 = 128×256 2 stages, 16 = 128×64 3 stages; < 0 = by shape.
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   if (a.A16) {  // bf16 A planes: the LDS-DMA tiles only (the forced / table tile, else the by-shape rule's)
+    // bf16 output rows (the bf16 variant's maps): the slab epilogue ("+ 100" → variant 3: res1 by LDS-DMA,
+    // rounded outputs staged as bf16 quads), bit-identical, 1.0-2.1x on every tile measured
+    // (profiles/r3/bf16/ab_slab_epilogue_bf16_rows.jsonl; launch_glds falls back where it does not apply)
+    const int ep = (planes == 1 && a.d.C_bf16) ? 100 : 0;
     if (cfg >= 11) {
-      const int rc = launch_glds_cfg(a, planes, cfg, s);
+      const int rc = launch_glds_cfg(a, planes, cfg < 100 ? cfg + ep : cfg, s);
       if (rc != -2) return rc;
     }
     int c = -1;
@@ -1369,7 +1373,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     else if (tiles(256, 128) >= 192) c = 12;
     else if (tiles(64, 128) >= 192) c = 13;
     else c = 14;
-    const int rc = launch_glds_cfg(a, planes, c, s);
+    const int rc = launch_glds_cfg(a, planes, c + ep, s);
     if (rc == -2) {
       set_error("sp_conv2d: no LDS-DMA tile for bf16 A planes");
       return -1;
@@ -1418,13 +1422,14 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
-  // The LDS-DMA residual epilogue (conv_glds.h epilogue_tile_rd, "cfg + 100") on the split mode's residual
-  // launches, for the tiles where it measured faster: 1.02-1.28x on the bottleneck expands (46, 45, 47, 14, 12,
-  // 63), 0.59-0.96x on the 256-wide-N / TN = 4 four-wave tiles (33, 44), bit-identical either way
-  // (profiles/r3/x3/ab_residual_dma_epilogue.jsonl)
-  if (planes == 3 && !a.A16 && a.d.res1 && !a.d.row_scale && a.vec_epi && a.splits == 1 && !a.d.C_bf16 &&
-      (cfg == 11 || cfg == 12 || cfg == 13 || cfg == 14 || cfg == 16 || cfg == 41 || cfg == 43 || cfg == 45 ||
-       cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64 || cfg == 65))
+  // The slab epilogue (conv_glds.h epilogue_tile_rd, "cfg + 100") on the split mode's launches with a BN affine
+  // or a residual, for the tiles where it measured faster, bit-identical either way: 1.02-1.28x on the
+  // bottleneck expands (the res1 band fetched by LDS-DMA; profiles/r3/x3/ab_residual_dma_epilogue.jsonl),
+  // 1.02-1.19x without a residual (the BN constants hoisted per lane; ab_slab_epilogue_nores.jsonl) on tiles
+  // 12, 14, 41, 45, 46, 47, 63, 64; 0.59-0.96x on the 256-wide-N / TN = 4 four-wave tiles (33, 44)
+  if (planes == 3 && !a.A16 && (a.d.res1 || a.d.scale || a.d.shift) && !a.d.row_scale && a.vec_epi &&
+      a.splits == 1 && !a.d.C_bf16 &&
+      (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
     cfg += 100;
   const int gc = cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;  // cfg + 100: the LDS-DMA residual epilogue variant
   if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {

@@ -44,6 +44,7 @@ EDGES = [(1, 1, 1000, 256, 192, True, "relu"), (3, 7, 9, 128, 320, False, None),
 
 PLANES = 3  # 3 = the fp32-accurate split (x3), 1 = the bf16 operand mode (--planes 1)
 VPL = False  # Winograd V as split bf16 planes (configuration suffix "v")
+BF16_ROWS = False  # --bf16-rows: activations / outputs / residuals as bf16 rows (with --planes 1)
 
 
 def force(c):
@@ -59,11 +60,15 @@ def make(dev, shape, seed=0):
     wino = shape[5] == "wino"
     k = 3 if wino else 1
     x = torch.randn(n * h * w * cin, device=dev, generator=g)
+    if BF16_ROWS:  # the bf16 variant's maps: bf16 rows in, bf16 rows out, bf16 residual rows
+        x = ((x.view(torch.int32) + 0x8000) >> 16).to(torch.int16)
     wt = torch.randn(cout * k * k * cin, device=dev, generator=g) * (1.0 / (cin * k * k) ** 0.5)
     sc = torch.rand(cout, device=dev, generator=g) + 0.5
     sh = torch.randn(cout, device=dev, generator=g)
-    out = torch.empty(n * h * w * cout, device=dev)
+    out = torch.empty(n * h * w * cout, device=dev, dtype=torch.int16 if BF16_ROWS else torch.float32)
     res = (torch.randn(n * h * w * cout, device=dev, generator=g) if shape[5] is True else None)
+    if BF16_ROWS and res is not None:
+        res = ((res.view(torch.int32) + 0x8000) >> 16).to(torch.int16)
     kw = {}
     if wino:
         u = ops.winograd_weights_host(wt.view(cout, 3, 3, cin).cpu().numpy(), 4)
@@ -111,9 +116,13 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--planes", type=int, default=3, choices=[1, 3])
     ap.add_argument("--no-check", action="store_true", help="skip the bit-identity check (pairs of different tiles)")
+    ap.add_argument("--bf16-rows", action="store_true", help="bf16 activation rows (the bf16 variant's maps)")
     a = ap.parse_args()
-    global PLANES
+    global PLANES, BF16_ROWS
     PLANES = a.planes
+    BF16_ROWS = a.bf16_rows
+    if BF16_ROWS and PLANES != 1:
+        raise SystemExit("--bf16-rows needs --planes 1")
     dev = torch.device("cuda", 0)
     pairs = [tuple(p.split(":")) for p in a.pairs.split(",")]
     lines = []
@@ -129,7 +138,7 @@ def main():
             res = []
             for c in (c0, c1):
                 force(c)
-                out.fill_(float("nan"))
+                out.fill_(-1 if BF16_ROWS else float("nan"))
                 try:
                     run()
                 except RuntimeError as e:
@@ -141,7 +150,7 @@ def main():
             if any(isinstance(r, str) for r in res):
                 emit({"check": list(shape), "pair": [c0, c1], "skipped": [r for r in res if isinstance(r, str)]})
                 continue
-            same = torch.equal(res[0], res[1]) and not torch.isnan(res[1]).any().item()
+            same = torch.equal(res[0], res[1]) and not (res[1].is_floating_point() and torch.isnan(res[1]).any().item())
             emit({"check": list(shape), "pair": [c0, c1], "planes": PLANES, "bit_identical": bool(same)})
             if not same:
                 raise SystemExit(f"variant {c1} differs from {c0} on {shape}")
