@@ -57,20 +57,26 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2));
 }
 
+// BF (template flag of the epilogue helpers below): the kernel may see bf16 rows (the bf16 operand mode's
+// kernels); the fp32-only kernels instantiate BF = false and carry no bf16 branches (sp_conv2d refuses bf16
+// rows outside the bf16 operand mode).
 // The res1 row segment n..n+3 of row m (fp32 or bf16 residual rows), zero without a residual.
+template <bool BF = false>
 __device__ __forceinline__ float4 load_res1(const sp_conv_desc& d, int64_t m, int n) {
-  if (d.res1_bf16) {
+  if (BF && d.res1_bf16) {
     const uint2 u = *reinterpret_cast<const uint2*>(d.res1_bf16 + m * d.ldr1 + n);
     return make_float4(bf16_lo(u.x), bf16_hi(u.x), bf16_lo(u.y), bf16_hi(u.y));
   }
   if (d.res1) return *reinterpret_cast<const float4*>(d.res1 + m * d.ldr1 + n);
   return make_float4(0.f, 0.f, 0.f, 0.f);
 }
-__device__ __forceinline__ bool has_res1(const sp_conv_desc& d) { return d.res1 || d.res1_bf16; }
+template <bool BF = false>
+__device__ __forceinline__ bool has_res1(const sp_conv_desc& d) { return d.res1 || (BF && d.res1_bf16); }
 
 // Store the finished float4 of row m, channels n..n+3 (fp32 rows or bf16 rows).
+template <bool BF = false>
 __device__ __forceinline__ void store_out4(const sp_conv_desc& d, int64_t m, int n, float4 v) {
-  if (d.C_bf16) {
+  if (BF && d.C_bf16) {
     *reinterpret_cast<uint2*>(d.C_bf16 + out_off(d, m) + n) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
   } else {
     *reinterpret_cast<float4*>(out_row(d, m) + n) = v;
@@ -79,6 +85,7 @@ __device__ __forceinline__ void store_out4(const sp_conv_desc& d, int64_t m, int
 
 // The fused epilogue on four consecutive output channels n..n+3 of row m (p.vec_epi, n+3 < Cout),
 // with the res1 row segment already loaded (r1; ignored when d.res1 is null).
+template <bool BF = false>
 __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n, float4 v, float4 r1) {
   const sp_conv_desc& d = p.d;
   if (d.row_scale) {
@@ -89,7 +96,7 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
   const float4 sh = d.shift ? *reinterpret_cast<const float4*>(d.shift + n) : make_float4(0.f, 0.f, 0.f, 0.f);
   v.x = fmaf(v.x, sc.x, sh.x); v.y = fmaf(v.y, sc.y, sh.y);
   v.z = fmaf(v.z, sc.z, sh.z); v.w = fmaf(v.w, sc.w, sh.w);
-  if (has_res1(d)) {
+  if (has_res1<BF>(d)) {
     v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
   }
   v.x = act_apply(v.x, d.act); v.y = act_apply(v.y, d.act);
@@ -97,18 +104,19 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
   if (d.res2) {
     const float4 a = *reinterpret_cast<const float4*>(d.res2 + m * d.ldr2 + n);
     v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-  } else if (d.res2_bf16) {
+  } else if (BF && d.res2_bf16) {
     const uint2 u = *reinterpret_cast<const uint2*>(d.res2_bf16 + m * d.ldr2 + n);
     v.x += bf16_lo(u.x); v.y += bf16_hi(u.x); v.z += bf16_lo(u.y); v.w += bf16_hi(u.y);
   }
-  store_out4(d, m, n, v);
+  store_out4<BF>(d, m, n, v);
 }
 
 // The fused epilogue on four consecutive output channels n..n+3 of row m.
+template <bool BF = false>
 __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int n, float4 v) {
   const sp_conv_desc& d = p.d;
   if (p.vec_epi && n + 3 < d.Cout) {
-    epilogue_vec(p, m, n, v, load_res1(d, m, n));
+    epilogue_vec<BF>(p, m, n, v, load_res1<BF>(d, m, n));
   } else {
     const int64_t ro = out_off(d, m);
     float e[4] = {v.x, v.y, v.z, v.w};
@@ -120,11 +128,11 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int
       if (d.row_scale) x *= d.row_scale[m % d.row_period];
       x = fmaf(x, d.scale ? d.scale[nn] : 1.0f, d.shift ? d.shift[nn] : 0.0f);
       if (d.res1) x += d.res1[m * d.ldr1 + nn];
-      if (d.res1_bf16) x += bf16_lo(d.res1_bf16[m * d.ldr1 + nn]);
+      if (BF && d.res1_bf16) x += bf16_lo(d.res1_bf16[m * d.ldr1 + nn]);
       x = act_apply(x, d.act);
       if (d.res2) x += d.res2[m * d.ldr2 + nn];
-      if (d.res2_bf16) x += bf16_lo(d.res2_bf16[m * d.ldr2 + nn]);
-      if (d.C_bf16) d.C_bf16[ro + nn] = (uint16_t)(pack_bf16x2(x, 0.f) & 0xffffu);
+      if (BF && d.res2_bf16) x += bf16_lo(d.res2_bf16[m * d.ldr2 + nn]);
+      if (BF && d.C_bf16) d.C_bf16[ro + nn] = (uint16_t)(pack_bf16x2(x, 0.f) & 0xffffu);
       else d.C[ro + nn] = x;
     }
   }
@@ -133,7 +141,7 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int
 // Accumulator band i of a wave (TN 32x32 MFMA tiles, v_mfma_f32_32x32x*: lane (r, h) holds
 // rows (q&3) + 8(q>>2) + 4h, column r) → the wave's private LDS slab → fused epilogue on
 // float4s of one output row (or raw partial sums for split-K).
-template <int TN>
+template <int TN, bool BF = false>
 __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, const f32x16* accrow,
                                               int64_t mb, int nb, int lane) {
   constexpr int WN = TN * 32;
@@ -157,7 +165,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
     if (p.splits > 1) {
       *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
     } else {
-      epilogue_store(p, m, n, v);
+      epilogue_store<BF>(p, m, n, v);
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -169,7 +177,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
 // region fits in the operand stages' LDS, else 1 (band by band).
 // L16: the f32x16 of each 32×32 block holds 2×2 blocks of v_mfma_f32_16x16x32 results (element
 // q = 8·bi + 4·bj + reg; lane l holds rows 16bi + 4(l >> 4) + reg, column 16bj + (l & 15)).
-template <int TM, int TN, int NB, bool L16 = false>
+template <int TM, int TN, int NB, bool L16 = false, bool BF = false>
 __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, f32x16 (*acc)[TN],
                                               int64_t mb, int nb, int lane) {
   static_assert(TM % NB == 0, "bands per round must divide TM");
@@ -206,7 +214,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         const int col = (cidx - row * (WN / 4)) * 4;
         const int64_t m = mr + row;
         const int n = nb + col;
-        r1[u] = (fastv && has_res1(d) && m < p.M && n < d.Cout) ? load_res1(d, m, n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        r1[u] = (fastv && has_res1<BF>(d) && m < p.M && n < d.Cout) ? load_res1<BF>(d, m, n) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int u = 0; u < G; ++u) {
@@ -220,9 +228,9 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         if (p.splits > 1) {
           *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
         } else if (fastv) {
-          epilogue_vec(p, m, n, v, r1[u]);
+          epilogue_vec<BF>(p, m, n, v, r1[u]);
         } else {
-          epilogue_store(p, m, n, v);
+          epilogue_store<BF>(p, m, n, v);
         }
       }
     }

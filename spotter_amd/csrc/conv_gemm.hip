@@ -312,6 +312,8 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
                    d->precision == SP_PREC_F32X3,
                "sp_conv2d: precision %d", d->precision);
   const int planes = d->precision == SP_PREC_BF16 ? 1 : d->precision == SP_PREC_F32X3 ? 3 : 0;
+  SP_ARG_CHECK(!(d->C_bf16 || d->res1_bf16 || d->res2_bf16) || planes == 1,
+               "sp_conv2d: bf16 output / residual rows need the bf16 operand mode (SP_PREC_BF16)");
   SP_ARG_CHECK(planes == 0 || d->Wt_bf16, "sp_conv2d: bf16 / split precision needs Wt_bf16");
   const int64_t K = (int64_t)d->KH * d->KW * d->Cin;
   SP_ARG_CHECK(planes < 3 || d->wt_plane_stride >= (int64_t)d->Cout * K,
@@ -364,7 +366,8 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     if (blocks64 < 64 && nk >= 8 && nk < 16) sp = nk / 4;
     else if (blocks64 < 256 && nk >= 16) sp = (int)((512 + blocks64 - 1) / blocks64), sp = sp < nk / 8 ? sp : nk / 8;
     else if (blocks64 < SP_SPLITK_BLOCKS && nk >= 64) sp = (int)((SP_SPLITK_BLOCKS + blocks64 - 1) / blocks64);
-    if (d->workspace && sp > 1 && !d->A_bf16) {  // split-K runs on the register-staged tiles (fp32 A)
+    // split-K runs on the register-staged tiles (fp32 A) and reduces through the fp32-row epilogue
+    if (d->workspace && sp > 1 && !d->A_bf16 && !d->C_bf16 && !d->res1_bf16 && !d->res2_bf16) {
       if (sp > 16) sp = 16;
       while (sp > 1 && (int64_t)sp * a.M * a.ldp > d->workspace_elems) --sp;
       if (sp > 1) a.splits = sp;

@@ -526,7 +526,7 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
   else if constexpr (EPV == 3)
     epilogue_tile_rd16<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
   else
-    epilogue_tile<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
+    epilogue_tile<TM, TN, C::NB, M16, PL == 1>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 }
 
 // OCC: minimum waves per SIMD the register allocation must allow (1 = unconstrained). Applied to the

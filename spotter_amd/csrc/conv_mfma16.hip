@@ -281,7 +281,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
   }
 
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
 }
 
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
 
   __syncthreads();
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
 }
 
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
 
   __syncthreads();
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
+  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
 }
 

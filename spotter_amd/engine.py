@@ -671,8 +671,10 @@ class Engine:
         for h, w in shapes[:-1]:
             starts.append(starts[-1] + h * w)
         # bf16 variant: source_flatten in bf16 — its two consumers are bf16-operand GEMMs (enc_output, the value
-        # projection) that round it to bf16 anyway, so this changes no result
-        src = self._buf("src_flat", B, S, D, dtype=torch.int16 if self.bf16_store else torch.float32)
+        # projection) that round it to bf16 anyway, so this changes no result ("bf16-convs" keeps it fp32: its
+        # linears run the fp32-accurate split)
+        src = self._buf("src_flat", B, S, D, dtype=torch.int16 if self.bf16_store and self._lin_mode == "bf16"
+                        else torch.float32)
         Hd = self.cfg.encoder_hidden_dim
         for l, (t, h, w) in enumerate(enc):
             self._cv(view(t, Hd), B, h, w, self.dec_proj[l], 1, V(src, starts[l] * D, D),
@@ -809,7 +811,8 @@ class Engine:
         # all six value projections at once (M2:190)
         L = cfg.decoder_layers
         # bf16 variant: the value projections stored as bf16 rows (sp_msda samples them in fp32)
-        vall = self._buf("value_all", rows, L * D, dtype=torch.int16 if self.bf16_store else torch.float32)
+        vall = self._buf("value_all", rows, L * D, dtype=torch.int16 if self.bf16_store and self._lin_mode == "bf16"
+                         else torch.float32)
         self._lin_op(view(src, D), rows, self.value_all, view(vall, L * D))
         # decoder (M2:578-661)
         nH, nL, nP = cfg.decoder_attention_heads, cfg.decoder_n_levels, cfg.decoder_n_points
