@@ -13,6 +13,9 @@
 #ifndef SP_GLDS_STAMP
 #define SP_GLDS_STAMP 0
 #endif
+#ifndef SP_GLDS_ONE_UNIT
+#define SP_GLDS_ONE_UNIT 0
+#endif
 
 namespace sp {
 

@@ -1,12 +1,12 @@
 // LDS-DMA implicit-GEMM kernels on bf16-operand MFMA (x3 split / bf16): the dispatcher of the tile
 // configurations 11-65 of launch_mfma16 (conv_mfma16.hip). The kernels live in conv_glds.h and are
-// instantiated across conv_glds_p<k>.hip; a diagnostic build (-DSP_GLDS_STAMP, tools/build_diag.sh)
-// instantiates them all here instead.
+// instantiated across conv_glds_p<k>.hip; a diagnostic build (tools/build_diag.sh: -DSP_GLDS_ONE_UNIT plus
+// -DSP_GLDS_STAMP or -DSP_ABLATE=n) instantiates them all here instead.
 #include "conv_glds.h"
 
 namespace sp {
 
-#if SP_GLDS_STAMP
+#if SP_GLDS_STAMP || SP_GLDS_ONE_UNIT
 namespace {
 int glds_part_k(int k, const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
   switch (k) {

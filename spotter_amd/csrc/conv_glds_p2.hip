@@ -2,7 +2,7 @@
 // translation unit so the build runs the parts in parallel.
 #include "conv_glds.h"
 
-#if !SP_GLDS_STAMP
+#if !(SP_GLDS_STAMP || SP_GLDS_ONE_UNIT)
 namespace sp {
 int launch_glds_part2(const ConvArgs& a, int planes, int cfg, hipStream_t s, int epv) {
   return glds_part<2>(a, planes, cfg, s, epv);

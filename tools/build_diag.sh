@@ -8,6 +8,6 @@ NAME=$1; shift
 mkdir -p spotter_amd/_diag
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=fast -Xarch_host -ffp-contract=off -munsafe-fp-atomics -Iinclude"
 OBJS=$(ls spotter_amd/_build/*.o | grep -v conv_glds)  # the diag unit instantiates every part itself
-/opt/rocm/bin/hipcc $F "$@" -c spotter_amd/csrc/conv_glds.hip -o spotter_amd/_diag/conv_glds_$NAME.o
+/opt/rocm/bin/hipcc $F -DSP_GLDS_ONE_UNIT=1 "$@" -c spotter_amd/csrc/conv_glds.hip -o spotter_amd/_diag/conv_glds_$NAME.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS spotter_amd/_diag/conv_glds_$NAME.o -o spotter_amd/_diag/libspotter_$NAME.so
 echo built spotter_amd/_diag/libspotter_$NAME.so

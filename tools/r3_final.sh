@@ -4,6 +4,14 @@ set -euo pipefail
 OUT=gpurun_out/${1:-r3f}; mkdir -p $OUT; export TMPDIR=/tmp
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/gpu_tests.log 2>&1
 tail -1 $OUT/gpu_tests.log
+if [ -d _ab_old ]; then  # same-box whole-bench A/B against the round-start tree
+  ARGS="--steps 10 --warmup 3 --no-cpu-baseline --latency-iters 0"
+  for i in 1 2; do
+    (cd _ab_old && timeout -k 10 240 python3 -u bench.py $ARGS) > $OUT/ab_old_$i.log 2>&1
+    timeout -k 10 240 python3 -u bench.py $ARGS > $OUT/ab_new_$i.log 2>&1
+    echo "A/B $i old $(tail -1 $OUT/ab_old_$i.log | cut -c100-125) new $(tail -1 $OUT/ab_new_$i.log | cut -c100-125)"
+  done
+fi
 timeout -k 10 420 python3 -u bench.py > $OUT/bench.log 2>&1
 tail -1 $OUT/bench.log | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-iters 0 > $OUT/prof.log 2>&1
