@@ -317,7 +317,8 @@ def conv_roofline(rec, cl, args, bf, rec_timed=None):
                 "f32": (1, "v_mfma_f32_32x32x2_f32", FP32_MFMA_PEAK_TFLOPS),
                 "f32+ln": (1, "v_mfma_f32_32x32x2_f32 (+ fused row LayerNorm)", FP32_MFMA_PEAK_TFLOPS),
                 "direct": (1, "v_fma_f32 (VALU stem conv, no MFMA)", FP32_MFMA_PEAK_TFLOPS),
-                "bf16-direct": (1, "v_mfma_f32_32x32x16_bf16 (direct LDS-halo stem 3x3)", BF16_MFMA_PEAK_TFLOPS)}
+                "bf16-direct": (1, "v_mfma_f32_32x32x16_bf16 (direct LDS-halo stem 3x3)", BF16_MFMA_PEAK_TFLOPS),
+                "f32-direct": (1, "v_mfma_f32_32x32x2_f32 (direct LDS-halo stem 3x3)", FP32_MFMA_PEAK_TFLOPS)}
     cm = rec.conv_modes()
     for md, c in cm.items():
         a = c["flops"] / (c["ms"] * 1e-3) / 1e12

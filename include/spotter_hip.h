@@ -203,6 +203,11 @@ int sp_stem_conv3x3s2_nchw_bf16(const float* x, const float* wt, const float* sc
  * in fp32, RNE at the store. Direct LDS-halo convolution (RN:78-103). */
 int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const float* scale, const float* shift, uint16_t* y,
                         int n, int h, int w, int cout, int act, void* stream);
+/* The same two convs on fp32 rows (ABI v10, the fp32 modes): dense NHWC fp32 rows in and out, weights fp32
+ * [Cout][3][3][32] (the packed [Cout][K] form), exact fp32 products with fp32 accumulation
+ * (v_mfma_f32_32x32x2_f32). Direct LDS-halo convolution (RN:78-103). */
+int sp_conv3x3_c32(const float* x, const float* wt, const float* scale, const float* shift, float* y, int n, int h,
+                   int w, int cout, int act, void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
  * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
 int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);

@@ -282,3 +282,177 @@ extern "C" int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const
                        w16, scale, shift, y, n, h, w, tiles_x, tiles_y, act);
   return check_launch("sp_conv3x3_c32_bf16");
 }
+
+// ---------------------------------------------------------------------------------------------
+// The same two stem convs in the fp32 modes (ABI v10): direct LDS-halo convolution on fp32 rows with
+// v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate). As fp32-MFMA implicit GEMMs they ran at
+// 93 / 106 TF of 157.3 (C2, profiles/r3/conv_detail_c2_fp32_r3g.json). One persistent workgroup per CU,
+// eight waves: the workgroup holds all 9·Cout·32 fp32 weights (36 / 72 KB) and one input halo of
+// (8 + 2) rows × (64 + 2) pixels × 32 channels (82.5 KB) in LDS; wave v computes output row v of the
+// tile (64 pixels × Cout) with the roles transposed as above (A = weights, B = pixels). The next tile's
+// halo is fetched into registers while the current one is computed. Channels: lane (r, half hh) reads a
+// float4 (4 consecutive channels of chunk 2q + hh) of its weight row and of its pixel; MFMA e of the four
+// takes component e, so MFMA e contracts channels 8q + e and 8q + 4 + e. LDS rows are 8 chunks of 16 B,
+// swizzled chunk ^ ((row >> 1) & 7): 16 consecutive rows' reads of one chunk land in 16 distinct slots.
+namespace sp {
+namespace {
+
+typedef float f32x4_s __attribute__((ext_vector_type(4)));
+
+constexpr int F3_TH = 8, F3_HR = F3_TH + 2, F3_HC = C3_TW + 2;
+constexpr int F3_HALO = F3_HR * F3_HC * 8;                  // 16-byte chunks of the halo
+constexpr int F3_PF = (F3_HALO + 511) / 512;                // halo chunks per thread
+
+__device__ __forceinline__ int f3_swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <int CO>
+__global__ __launch_bounds__(512, 1) void conv3x3_c32_f32_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ wt,
+                                                                 const float* __restrict__ scale,
+                                                                 const float* __restrict__ shift,
+                                                                 float* __restrict__ y, int nimg, int h, int w,
+                                                                 int tiles_x, int tiles_y, int act) {
+  constexpr int WCH = 9 * CO * 8;  // 16-byte chunks of the weights
+  constexpr int TMN = CO / 32;
+  __shared__ uint4 lds[F3_HALO + WCH];
+  __shared__ float aff[2 * CO];  // the BN affine: per-tile global loads of it would wait behind the prefetch
+  uint4* halo = lds;
+  uint4* wl = lds + F3_HALO;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < CO) {
+    aff[tid] = scale[tid];
+    aff[CO + tid] = shift[tid];
+  }
+  // weights: global [CO][9 taps][32 ci] fp32 (the packed [Cout][K] form) → LDS [tap][n][chunk ^ swz(n)]
+  for (int i = tid; i < WCH; i += 512) {
+    const int c = i & 7, tn = i >> 3, n = tn / 9, tap = tn - n * 9;
+    wl[(tap * CO + n) * 8 + f3_swz(n, c)] = *reinterpret_cast<const uint4*>(wt + (int64_t)i * 4);
+  }
+  const int64_t ntiles = (int64_t)nimg * tiles_x * tiles_y;
+  uint4 pf[F3_PF];
+  unsigned okm = 0;  // bit k: pf[k] is inside the map (out-of-map chunks are loaded from x[0] and zeroed at the stash)
+  // fetch tile t's halo (rows oy0-1 .. oy0+8, pixels ox0-1 .. ox0+64; zero outside the map) into registers:
+  // unconditional loads, so no wait for them is needed before the MFMAs that follow
+  auto fetch = [&](int64_t t) {
+    const int tx = (int)(t % tiles_x);
+    t /= tiles_x;
+    const int ty = (int)(t % tiles_y);
+    const int b = (int)(t / tiles_y);
+    const int oy0 = ty * F3_TH, ox0 = tx * C3_TW;
+#pragma unroll
+    for (int k = 0; k < F3_PF; ++k) {
+      const int i = tid + k * 512;
+      const int c = i & 7, rc = i >> 3, r = rc / F3_HC, col = rc - r * F3_HC;
+      const int iy = oy0 - 1 + r, ix = ox0 - 1 + col;
+      const bool ok = i < F3_HALO && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      const int64_t off = ok ? (((int64_t)b * h + iy) * w + ix) * 32 + c * 4 : 0;
+      pf[k] = *reinterpret_cast<const uint4*>(x + off);
+      okm = k == 0 ? (unsigned)ok : (okm | ((unsigned)ok << k));
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int k = 0; k < F3_PF; ++k) {
+      const int i = tid + k * 512;
+      if (i < F3_HALO) {
+        const int c = i & 7, rc = i >> 3, col = rc % F3_HC;
+        halo[rc * 8 + f3_swz(col, c)] = (okm >> k) & 1u ? pf[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x < ntiles) fetch(blockIdx.x);
+  const int r = lane & 31, hh = lane >> 5;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's halo reads are done
+    stash();
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);  // overlaps the MFMAs below
+    int64_t t = tile;
+    const int tx = (int)(t % tiles_x);
+    t /= tiles_x;
+    const int ty = (int)(t % tiles_y);
+    const int b = (int)(t / tiles_y);
+    const int oy = ty * F3_TH + wave, ox0 = tx * C3_TW;
+    f32x16_s acc[TMN][2];
+#pragma unroll
+    for (int i = 0; i < TMN; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = 2 * q + hh;  // chunk: ci 8q + 4hh .. +3
+          f32x4_s fa[TMN], fb[2];
+#pragma unroll
+          for (int i = 0; i < TMN; ++i) {
+            const int n = i * 32 + r;
+            fa[i] = *reinterpret_cast<const f32x4_s*>(wl + (tap * CO + n) * 8 + f3_swz(n, ch));
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int col = j * 32 + r + kw;
+            fb[j] = *reinterpret_cast<const f32x4_s*>(halo + ((wave + kh) * F3_HC + col) * 8 + f3_swz(col, ch));
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < TMN; ++i)
+#pragma unroll
+              for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][e], fb[j][e], acc[i][j], 0, 0, 0);
+        }
+      }
+    // epilogue: lane (pixel r of block j, half hh) holds channels i·32 + 8g + 4hh .. +3 in acc[i][j][4g .. 4g+3]
+    if (oy < h) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ox = ox0 + j * 32 + r;
+        if (ox >= w) continue;
+        float* yrow = y + (((int64_t)b * h + oy) * w + ox) * CO;
+#pragma unroll
+        for (int i = 0; i < TMN; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n0 = i * 32 + 8 * g + 4 * hh;
+            float4 v;
+            float* vv = &v.x;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[CO + n0 + e]);
+              vv[e] = act ? fmaxf(u, 0.f) : u;
+            }
+            *reinterpret_cast<float4*>(yrow + n0) = v;
+          }
+      }
+    }
+  }  // tiles
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_conv3x3_c32(const float* x, const float* wt, const float* scale, const float* shift, float* y,
+                              int n, int h, int w, int cout, int act, void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(x && wt && scale && shift && y && n > 0 && h > 0 && w > 0 && (cout == 32 || cout == 64) &&
+                   (act == 0 || act == 1) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)wt & 15) == 0 &&
+                   ((uintptr_t)y & 15) == 0,
+               "sp_conv3x3_c32: bad args (Cin 32, Cout 32 or 64, act none/relu, aligned dense fp32 rows)");
+  const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + F3_TH - 1) / F3_TH;
+  const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
+  const unsigned grid = (unsigned)(tiles < g_num_cus ? tiles : g_num_cus);  // persistent: one per CU
+  if (cout == 32)
+    hipLaunchKernelGGL((conv3x3_c32_f32_kernel<32>), dim3(grid), dim3(512), 0, as_stream(stream), x, wt, scale,
+                       shift, y, n, h, w, tiles_x, tiles_y, act);
+  else
+    hipLaunchKernelGGL((conv3x3_c32_f32_kernel<64>), dim3(grid), dim3(512), 0, as_stream(stream), x, wt, scale,
+                       shift, y, n, h, w, tiles_x, tiles_y, act);
+  return check_launch("sp_conv3x3_c32");
+}

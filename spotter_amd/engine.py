@@ -151,7 +151,7 @@ class Engine:
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
                  fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False,
-                 bf16_store: bool | None = None):
+                 bf16_store: bool | None = None, direct_c32: bool = True):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -198,6 +198,9 @@ class Engine:
         self.bf16_store = (self._conv_mode == "bf16") if bf16_store is None else bool(bf16_store)
         if self.bf16_store and self._conv_mode != "bf16":
             raise ValueError("bf16_store needs a bf16 conv operand mode")
+        # the Cin-32 stem 3x3s on fp32-MFMA weights as the direct LDS-halo kernel (sp_conv3x3_c32) instead of
+        # the fp32-MFMA implicit GEMM
+        self.direct_c32 = direct_c32
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -476,6 +479,8 @@ class Engine:
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                           row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
+    C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)
+
     def _direct_stem(self) -> bool:
         """The stem's first conv (Cin 3, K = 27) runs on the direct NCHW kernel (sp_stem_conv3x3s2_nchw, fp32
         weights, exact fmaf chains) in every precision mode: K = 27 gives a GEMM nothing to tile (the bf16
@@ -504,11 +509,20 @@ class Engine:
             ops.nchw_to_nhwc(pixel_values, px)
             self._cv(view(px, 3), B, H, W, c0, 2, view(s0, e // 2), act=self.act_bb)
         for src, cw, dst in ((s0, self.stem[1], s1), (s1, self.stem[2], s2)):
-            if self.bf16_store and cw.cin == 32 and cw.k == 3 and cw.cout in (32, 64) and self.act_bb in ("relu", None):
+            c32 = cw.cin == 32 and cw.k == 3 and cw.cout in (32, 64) and self.act_bb in ("relu", None)
+            if c32 and self.bf16_store:
                 # the bf16 variant's Cin-32 stem 3×3s: direct LDS-halo kernel (the implicit GEMM re-fetched every
                 # A row per tap and wasted half a 64-wide tile on Cout 32)
                 ops.conv3x3_c32_bf16(view(src, cw.cin), cw.w16, cw.scale, cw.shift, view(dst, cw.cout), B, h1, w1,
                                      cw.cout, act=self.act_bb)
+            elif (c32 and self.direct_c32 and cw.mode == "f32" and not self.bf16_store
+                  and B * h1 * w1 >= self.C32_MIN_PIXELS):
+                # the fp32 modes: the same direct kernel on fp32 rows with fp32 MFMAs (exact products): 1.24-1.29x
+                # the fp32-MFMA GEMM at bs32 (113 / 128 TF), 1.08-1.17x at bs8 of 320²
+                # (profiles/r3/x3/ab_stem_c32_f32.jsonl); smaller maps (a few tiles per CU at most for its
+                # one-workgroup-per-CU grid) keep the GEMM
+                ops.conv3x3_c32(view(src, cw.cin), cw.w, cw.scale, cw.shift, view(dst, cw.cout), B, h1, w1, cw.cout,
+                                act=self.act_bb)
             else:
                 self._cv(view(src, cw.cin), B, h1, w1, cw, 1, view(dst, cw.cout), act=self.act_bb)
         h, w = (h1 - 1) // 2 + 1, (w1 - 1) // 2 + 1

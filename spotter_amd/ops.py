@@ -341,6 +341,22 @@ def conv3x3_c32_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.
             2 * m * cout * 288, 2 * (m * 32 + cout * 288 + m * cout), (m, cout, 288, 3, 1, "bf16-direct"))
 
 
+def conv3x3_c32(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int, w: int,
+                cout: int, act=None):
+    """Stem convs 2 / 3 in the fp32 modes (RN:78-103: 3×3/1, Cin 32 → Cout 32 or 64, FrozenBN, ReLU) on dense
+    fp32 NHWC rows: the direct LDS-halo kernel sp_conv3x3_c32 (fp32 MFMA)."""
+    if x.is_bf16 or y.is_bf16 or x.ld != 32 or y.ld != cout:
+        raise ValueError("conv3x3_c32: dense fp32 rows (ld 32 in, Cout out) expected")
+    if wt.dtype != torch.float32 or wt.numel() != cout * 288 or scale.numel() < cout or shift.numel() < cout:
+        raise ValueError("conv3x3_c32: weight / affine size mismatch")
+    m = n * h * w
+    xp = x.need(m, 32, "c32.x")
+    yp = y.need(m, cout, "c32.y")
+    _launch("conv", "sp_conv3x3_c32", (xp, wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, n, h, w, cout,
+                                       ACT[act], stream()),
+            2 * m * cout * 288, 4 * (m * 32 + cout * 288 + m * cout), (m, cout, 288, 3, 1, "f32-direct"))
+
+
 def _pool_out(y, m: int, c: int, what: str):
     """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
     if isinstance(y, V):

@@ -460,6 +460,42 @@ def test_conv3x3_c32_bf16_direct(dev, cout, act, hw):
     assert np.array_equal(out.cpu().numpy(), ref.cpu().numpy())
 
 
+@pytest.mark.parametrize("cout,act,hw", [(32, "relu", (13, 70)), (64, "relu", (9, 129)), (64, None, (4, 64)),
+                                         (32, None, (1, 1)), (64, "relu", (17, 200))])
+def test_conv3x3_c32_f32_direct(dev, cout, act, hw):
+    """sp_conv3x3_c32 (the fp32 modes' direct stem 3×3, ABI v10) against the fp32-MFMA implicit GEMM and an
+    fp64 conv: exact fp32 products, fp32 accumulation in another order, so within a few fp32 roundings of the
+    288-term sums (3e-6 of the output scale; the GEMM's own error sets the bar). Ragged tile edges in both
+    directions, one-pixel maps, more tiles than CUs' worth of rows (the persistent loop's prefetch)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(61 + cout)
+    n, (h, w) = 2, hw
+    m = n * h * w
+    x = rng.standard_normal((n, h, w, 32)).astype(np.float32)
+    wt = (rng.standard_normal((cout, 3, 3, 32)) / 17).astype(np.float32)
+    sc, sh = rng.uniform(0.5, 1.5, cout).astype(np.float32), rng.standard_normal(cout).astype(np.float32)
+    xd, wd, scd, shd = T(x.reshape(-1), dev), T(wt.reshape(cout, 288), dev), T(sc, dev), T(sh, dev)
+    ref = torch.empty(m * cout, device=dev)
+    ops.conv2d(V(xd, 0, 32), n, h, w, 32, wd, cout, 3, 1, 1, V(ref, 0, cout), scale=scd, shift=shd, act=act)
+    out = torch.full((m * cout,), float("nan"), device=dev)
+    ops.conv3x3_c32(V(xd, 0, 32), wd, scd, shd, V(out, 0, cout), n, h, w, cout, act=act)
+    got = out.cpu().numpy().reshape(n, h, w, cout)
+    xp = np.pad(x.astype(np.float64), ((0, 0), (1, 1), (1, 1), (0, 0)))
+    acc = np.zeros((n, h, w, cout))
+    for kh in range(3):
+        for kw in range(3):
+            acc += xp[:, kh:kh + h, kw:kw + w, :] @ wt[:, kh, kw, :].astype(np.float64).T
+    want = acc * sc + sh
+    if act:
+        want = np.maximum(want, 0)
+    tol = 3e-6 * np.abs(want).max()
+    assert np.isfinite(got).all()
+    assert np.abs(got - want).max() <= tol
+    assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, cout)).max() <= tol
+
+
 def test_pools_and_stem_bf16_rows(dev):
     """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32
     kernels on the same bf16-representable inputs with the result rounded to bf16 (max: exact)."""
