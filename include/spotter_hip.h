@@ -208,6 +208,12 @@ int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const float* sca
  * (v_mfma_f32_32x32x2_f32). Direct LDS-halo convolution (RN:78-103). */
 int sp_conv3x3_c32(const float* x, const float* wt, const float* scale, const float* shift, float* y, int n, int h,
                    int w, int cout, int act, void* stream);
+/* The ResNet stage-0 3x3 (Cin 64 → Cout 64, stride 1 pad 1, RN:170-231) in the fp32 modes: fp32 NHWC rows ldx /
+ * ldy floats apart (>= 64, % 4, 16-byte aligned: y may be a channel slice of a wider buffer), weights fp32
+ * [64][3][3][64], FrozenBN (scale, shift) + act, exact fp32 products (v_mfma_f32_32x32x2_f32). Direct LDS-halo
+ * convolution. */
+int sp_conv3x3_c64(const float* x, int64_t ldx, const float* wt, const float* scale, const float* shift, float* y,
+                   int64_t ldy, int n, int h, int w, int act, void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
  * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
 int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);

@@ -151,7 +151,7 @@ class Engine:
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
                  fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False,
-                 bf16_store: bool | None = None, direct_c32: bool = True):
+                 bf16_store: bool | None = None, direct_c32: bool = True, direct_c64: bool = False):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -201,6 +201,7 @@ class Engine:
         # the Cin-32 stem 3x3s on fp32-MFMA weights as the direct LDS-halo kernel (sp_conv3x3_c32) instead of
         # the fp32-MFMA implicit GEMM
         self.direct_c32 = direct_c32
+        self.direct_c64 = direct_c64  # the stage-0 3x3 (Cin 64 -> 64) likewise (sp_conv3x3_c64)
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -446,6 +447,11 @@ class Engine:
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
+        if (self.direct_c64 and cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw
+                and res1 is None and res2 is None and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32")
+                and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
+            # the stage-0 3x3 of the fp32 modes: direct LDS-halo kernel, exact fp32 products (sp_conv3x3_c64)
+            return ops.conv3x3_c64(x, cw.w, cw.scale, cw.shift, out, n, h, w, act=act)
         if cw.wino is not None and stride == 1 and not kw and not x.is_bf16 and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
@@ -479,6 +485,7 @@ class Engine:
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                           row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
+    C64_MIN_PIXELS = 1 << 18
     C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)
 
     def _direct_stem(self) -> bool:

@@ -357,6 +357,22 @@ def conv3x3_c32(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor
             2 * m * cout * 288, 4 * (m * 32 + cout * 288 + m * cout), (m, cout, 288, 3, 1, "f32-direct"))
 
 
+def conv3x3_c64(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int, w: int,
+                act=None):
+    """The ResNet stage-0 3×3 in the fp32 modes (RN:170-231: 3×3/1, Cin 64 → Cout 64, FrozenBN, act) on fp32 NHWC
+    rows (x and y may be channel slices of wider buffers): the direct LDS-halo kernel sp_conv3x3_c64."""
+    if x.is_bf16 or y.is_bf16 or x.ld % 4 or y.ld % 4 or x.off % 4 or y.off % 4:
+        raise ValueError("conv3x3_c64: 16-byte aligned fp32 row views expected")
+    if wt.dtype != torch.float32 or wt.numel() != 64 * 576 or scale.numel() < 64 or shift.numel() < 64:
+        raise ValueError("conv3x3_c64: weight / affine size mismatch")
+    m = n * h * w
+    xp = x.need(m, 64, "c64.x")
+    yp = y.need(m, 64, "c64.y")
+    _launch("conv", "sp_conv3x3_c64", (xp, x.ld, wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, y.ld, n, h,
+                                       w, ACT[act], stream()),
+            2 * m * 64 * 576, 4 * (m * 64 + 64 * 576 + m * 64), (m, 64, 576, 3, 1, "f32-direct"))
+
+
 def _pool_out(y, m: int, c: int, what: str):
     """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
     if isinstance(y, V):

@@ -496,6 +496,49 @@ def test_conv3x3_c32_f32_direct(dev, cout, act, hw):
     assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, cout)).max() <= tol
 
 
+@pytest.mark.parametrize("act,hw,lds", [("relu", (13, 70), (64, 64)), (None, (5, 129), (128, 192)),
+                                        ("relu", (1, 1), (64, 128)), ("relu", (40, 64), (64, 64))])
+def test_conv3x3_c64_f32_direct(dev, act, hw, lds):
+    """sp_conv3x3_c64 (the fp32 modes' stage-0 3×3, Cin 64 → 64) against an fp64 conv and the fp32-MFMA
+    implicit GEMM, within 3e-6 of the output scale; input / output as channel slices of wider rows (the fused
+    bottleneck tail's layout), ragged tiles, one-pixel maps, more tiles than workgroups; the columns around
+    the output slice stay untouched."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(71)
+    n, (h, w) = 2, hw
+    ldx, ldy = lds
+    m = n * h * w
+    x = rng.standard_normal((n, h, w, 64)).astype(np.float32)
+    xrows = np.zeros((m, ldx), np.float32)
+    xrows[:, ldx - 64:] = x.reshape(m, 64)
+    wt = (rng.standard_normal((64, 3, 3, 64)) / 24).astype(np.float32)
+    sc, sh = rng.uniform(0.5, 1.5, 64).astype(np.float32), rng.standard_normal(64).astype(np.float32)
+    xd, wd, scd, shd = T(xrows.reshape(-1), dev), T(wt.reshape(64, 576), dev), T(sc, dev), T(sh, dev)
+    xv = V(xd, ldx - 64, ldx)
+    ref = torch.empty(m * 64, device=dev)
+    ops.conv2d(xv, n, h, w, 64, wd, 64, 3, 1, 1, V(ref, 0, 64), scale=scd, shift=shd, act=act)
+    out = torch.full((m * ldy,), float("nan"), device=dev)
+    yo = ldy - 64
+    ops.conv3x3_c64(xv, wd, scd, shd, V(out, yo, ldy), n, h, w, act=act)
+    rows = out.cpu().numpy().reshape(m, ldy)
+    got = rows[:, yo:].reshape(n, h, w, 64)
+    assert np.isnan(rows[:, :yo]).all()
+    xp = np.pad(x.astype(np.float64), ((0, 0), (1, 1), (1, 1), (0, 0)))
+    acc = np.zeros((n, h, w, 64))
+    for kh in range(3):
+        for kw in range(3):
+            acc += xp[:, kh:kh + h, kw:kw + w, :] @ wt[:, kh, kw, :].astype(np.float64).T
+    want = acc * sc + sh
+    if act:
+        want = np.maximum(want, 0)
+    tol = 3e-6 * np.abs(want).max()
+    assert np.isfinite(got).all()
+    assert np.abs(got - want).max() <= tol
+    assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, 64)).max() <= tol
+
+
 def test_pools_and_stem_bf16_rows(dev):
     """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32
     kernels on the same bf16-representable inputs with the result rounded to bf16 (max: exact)."""
