@@ -629,3 +629,154 @@ extern "C" int sp_conv3x3_c64(const float* x, int64_t ldx, const float* wt, cons
                      as_stream(stream), x, wt, scale, shift, y, ldx, ldy, n, h, w, tiles_x, tiles_y, act);
   return check_launch("sp_conv3x3_c64");
 }
+
+// ---------------------------------------------------------------------------------------------
+// The stage-0 3×3 (Cin 64 → Cout 64) of the bf16 variant on bf16 rows: the Cin-32 kernel above with 64-channel
+// rows (8 chunks of 16 B, swizzled chunk ^ ((row >> 1) & 7)), all 9·64·64 bf16 weights (73.7 KB) and an
+// (8 + 2) × 66 × 64 bf16 halo (84.5 KB) in LDS, eight waves (one output row each), rows ldx / ldy elements
+// apart (the fused bottleneck tail reads this output as a channel slice). Sums the 576-deep k in (tap,
+// 16-channel) order with v_mfma_f32_32x32x16_bf16 blocks, as the implicit GEMM does.
+namespace sp {
+namespace {
+
+constexpr int B6_TH = 8, B6_HR = B6_TH + 2, B6_HC = C3_TW + 2;
+constexpr int B6_HALO = B6_HR * B6_HC * 8;   // 16-byte chunks of the halo
+constexpr int B6_WCH = 9 * 64 * 8;           // 16-byte chunks of the weights
+constexpr int B6_PF = (B6_HALO + 511) / 512;  // halo chunks per thread
+
+__global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t* __restrict__ x,
+                                                                  const uint16_t* __restrict__ w16,
+                                                                  const float* __restrict__ scale,
+                                                                  const float* __restrict__ shift,
+                                                                  uint16_t* __restrict__ y, int64_t ldx,
+                                                                  int64_t ldy, int nimg, int h, int w, int tiles_x,
+                                                                  int tiles_y, int act) {
+  __shared__ uint4 lds[B6_HALO + B6_WCH];
+  __shared__ float aff[128];
+  uint4* halo = lds;
+  uint4* wl = lds + B6_HALO;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // weights: global [64][9 taps][64 ci] bf16 → LDS [tap][n][chunk ^ swz(n)]
+  for (int i = tid; i < B6_WCH; i += 512) {
+    const int c = i & 7, tn = i >> 3, n = tn / 9, tap = tn - n * 9;
+    wl[(tap * 64 + n) * 8 + f3_swz(n, c)] = *reinterpret_cast<const uint4*>(w16 + (int64_t)i * 8);
+  }
+  if (tid < 64) {
+    aff[tid] = scale[tid];
+    aff[64 + tid] = shift[tid];
+  }
+  const int64_t ntiles = (int64_t)nimg * tiles_x * tiles_y;
+  uint4 pf[B6_PF];
+  unsigned okm = 0;
+  auto fetch = [&](int64_t t) {
+    const int tx = (int)(t % tiles_x);
+    t /= tiles_x;
+    const int ty = (int)(t % tiles_y);
+    const int b = (int)(t / tiles_y);
+    const int oy0 = ty * B6_TH, ox0 = tx * C3_TW;
+#pragma unroll
+    for (int k = 0; k < B6_PF; ++k) {
+      const int i = tid + k * 512;
+      const int c = i & 7, rc = i >> 3, r = rc / B6_HC, col = rc - r * B6_HC;
+      const int iy = oy0 - 1 + r, ix = ox0 - 1 + col;
+      const bool ok = i < B6_HALO && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
+      const int64_t off = ok ? (((int64_t)b * h + iy) * w + ix) * ldx + c * 8 : 0;
+      pf[k] = *reinterpret_cast<const uint4*>(x + off);
+      okm = k == 0 ? (unsigned)ok : (okm | ((unsigned)ok << k));
+    }
+  };
+  if ((int64_t)blockIdx.x < ntiles) fetch(blockIdx.x);
+  const int r = lane & 31, hh = lane >> 5;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's halo reads are done
+#pragma unroll
+    for (int k = 0; k < B6_PF; ++k) {
+      const int i = tid + k * 512;
+      if (i < B6_HALO) {
+        const int c = i & 7, rc = i >> 3, col = rc % B6_HC;
+        halo[rc * 8 + f3_swz(col, c)] = (okm >> k) & 1u ? pf[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);  // overlaps the MFMAs below
+    int64_t t = tile;
+    const int tx = (int)(t % tiles_x);
+    t /= tiles_x;
+    const int ty = (int)(t % tiles_y);
+    const int b = (int)(t / tiles_y);
+    const int oy = ty * B6_TH + wave, ox0 = tx * C3_TW;
+    f32x16_s acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[i][j][q] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int tap = kh * 3 + kw;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ch = 2 * s + hh;  // k chunk: ci 16s + 8hh .. +7
+          bf16x8_s fa[2], fb[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int n = i * 32 + r;
+            fa[i] = *reinterpret_cast<const bf16x8_s*>(wl + (tap * 64 + n) * 8 + f3_swz(n, ch));
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int col = j * 32 + r + kw;
+            fb[j] = *reinterpret_cast<const bf16x8_s*>(halo + ((wave + kh) * B6_HC + col) * 8 + f3_swz(col, ch));
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      }
+    if (oy < h) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ox = ox0 + j * 32 + r;
+        if (ox >= w) continue;
+        uint16_t* yrow = y + (((int64_t)b * h + oy) * w + ox) * ldy;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int n0 = i * 32 + 8 * g + 4 * hh;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
+              v[e] = act ? fmaxf(u, 0.f) : u;
+            }
+            *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+          }
+      }
+    }
+  }  // tiles
+}
+
+}  // namespace
+}  // namespace sp
+
+extern "C" int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_t* w16, const float* scale,
+                                   const float* shift, uint16_t* y, int64_t ldy, int n, int h, int w, int act,
+                                   void* stream) {
+  using namespace sp;
+  SP_ARG_CHECK(x && w16 && scale && shift && y && n > 0 && h > 0 && w > 0 && (act == 0 || act == 1) &&
+                   ldx >= 64 && ldy >= 64 && ldx % 8 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 7) == 0,
+               "sp_conv3x3_c64_bf16: bad args (act none/relu, aligned bf16 rows, ldx % 8, ldy % 4, ld >= 64)");
+  const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + B6_TH - 1) / B6_TH;
+  const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
+  const unsigned grid = (unsigned)(tiles < g_num_cus ? tiles : g_num_cus);  // persistent: one per CU
+  hipLaunchKernelGGL(conv3x3_c64_bf16_kernel, dim3(grid), dim3(512), 0, as_stream(stream), x, w16, scale, shift, y,
+                     ldx, ldy, n, h, w, tiles_x, tiles_y, act);
+  return check_launch("sp_conv3x3_c64_bf16");
+}

@@ -151,7 +151,8 @@ class Engine:
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
                  fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False,
-                 bf16_store: bool | None = None, direct_c32: bool = True, direct_c64: bool = False):
+                 bf16_store: bool | None = None, direct_c32: bool = True, direct_c64: bool = False,
+                 direct_c64_bf16: bool = True):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -202,6 +203,7 @@ class Engine:
         # the fp32-MFMA implicit GEMM
         self.direct_c32 = direct_c32
         self.direct_c64 = direct_c64  # the stage-0 3x3 (Cin 64 -> 64) likewise (sp_conv3x3_c64)
+        self.direct_c64_bf16 = direct_c64_bf16  # and on bf16 rows (sp_conv3x3_c64_bf16)
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -447,11 +449,15 @@ class Engine:
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        if (self.direct_c64 and cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw
-                and res1 is None and res2 is None and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32")
-                and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
-            # the stage-0 3x3 of the fp32 modes: direct LDS-halo kernel, exact fp32 products (sp_conv3x3_c64)
-            return ops.conv3x3_c64(x, cw.w, cw.scale, cw.shift, out, n, h, w, act=act)
+        if (cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw and res1 is None
+                and res2 is None and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
+            if self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16":
+                # the bf16 variant's stage-0 3x3: direct LDS-halo kernel, bit-identical to the implicit GEMM and
+                # 1.53x it at bs32 / bs256 (814 TF at C3; profiles/r3/bf16/ab_conv3x3_c64_bf16.jsonl)
+                return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act)
+            if self.direct_c64 and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32"):
+                # the fp32 modes' form (sp_conv3x3_c64): slower than the split GEMM today, off by default
+                return ops.conv3x3_c64(x, cw.w, cw.scale, cw.shift, out, n, h, w, act=act)
         if cw.wino is not None and stride == 1 and not kw and not x.is_bf16 and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)

@@ -373,6 +373,22 @@ def conv3x3_c64(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor
             2 * m * 64 * 576, 4 * (m * 64 + 64 * 576 + m * 64), (m, 64, 576, 3, 1, "f32-direct"))
 
 
+def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int,
+                     w: int, act=None):
+    """The stage-0 3×3 of the bf16 variant (Cin 64 → 64) on bf16 rows (channel-slice views allowed): the direct
+    LDS-halo kernel sp_conv3x3_c64_bf16."""
+    if not (x.is_bf16 and y.is_bf16) or x.ld % 8 or x.off % 8 or y.ld % 4 or y.off % 4:
+        raise ValueError("conv3x3_c64_bf16: aligned bf16 row views expected")
+    if w16.dtype != torch.int16 or w16.numel() != 64 * 576 or scale.numel() < 64 or shift.numel() < 64:
+        raise ValueError("conv3x3_c64_bf16: weight / affine size mismatch")
+    m = n * h * w
+    xp = x.need(m, 64, "c64b.x", bf16=True)
+    yp = y.need(m, 64, "c64b.y", bf16=True)
+    _launch("conv", "sp_conv3x3_c64_bf16", (xp, x.ld, w16.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, y.ld,
+                                            n, h, w, ACT[act], stream()),
+            2 * m * 64 * 576, 2 * (m * 64 + 64 * 576 + m * 64), (m, 64, 576, 3, 1, "bf16-direct"))
+
+
 def _pool_out(y, m: int, c: int, what: str):
     """y: a dense tensor or a V row view (a channel slice of a wider buffer) → (ptr, ldy)."""
     if isinstance(y, V):

@@ -539,6 +539,39 @@ def test_conv3x3_c64_f32_direct(dev, act, hw, lds):
     assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, 64)).max() <= tol
 
 
+@pytest.mark.parametrize("act,hw,lds", [("relu", (13, 70), (64, 64)), (None, (9, 129), (128, 192)),
+                                        ("relu", (1, 1), (64, 128)), ("relu", (40, 64), (64, 64))])
+def test_conv3x3_c64_bf16_direct(dev, act, hw, lds):
+    """sp_conv3x3_c64_bf16 (the bf16 variant's stage-0 3×3) equals the implicit-GEMM bf16 path on the same
+    bf16 rows bit for bit (both sum the 576-deep k in (tap, 16-channel) order with v_mfma_f32_32x32x16_bf16
+    blocks); channel-slice input / output rows, ragged tiles, one-pixel maps; columns around the slice kept."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(81)
+    n, (h, w) = 2, hw
+    ldx, ldy = lds
+    m = n * h * w
+    x16, _ = _bf16_rows(rng.standard_normal((m, 64)).astype(np.float32))
+    xrows = np.zeros((m, ldx), np.int16)
+    xrows[:, ldx - 64:] = x16.reshape(m, 64)
+    wt = (rng.standard_normal((64, 576)) / 24).astype(np.float32)
+    w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
+    sc, sh = T(rng.uniform(0.5, 1.5, 64).astype(np.float32), dev), T(rng.standard_normal(64).astype(np.float32), dev)
+    xv = V(T(xrows.reshape(-1), dev), ldx - 64, ldx)
+    ref = torch.full((m * 64,), -1, dtype=torch.int16, device=dev)
+    ops.force_conv_config("14")
+    try:
+        ops.conv2d(xv, n, h, w, 64, T(wt, dev), 64, 3, 1, 1, V(ref, 0, 64), scale=sc, shift=sh, act=act, wt16=w16)
+    finally:
+        ops.force_conv_config(None)
+    out = torch.full((m * ldy,), -1, dtype=torch.int16, device=dev)
+    ops.conv3x3_c64_bf16(xv, w16, sc, sh, V(out, ldy - 64, ldy), n, h, w, act=act)
+    rows = out.cpu().numpy().reshape(m, ldy)
+    assert np.all(rows[:, :ldy - 64] == -1)
+    assert np.array_equal(rows[:, ldy - 64:], ref.cpu().numpy().reshape(m, 64))
+
+
 def test_pools_and_stem_bf16_rows(dev):
     """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32
     kernels on the same bf16-representable inputs with the result rounded to bf16 (max: exact)."""
