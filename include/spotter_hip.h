@@ -215,9 +215,11 @@ int sp_conv3x3_c32(const float* x, const float* wt, const float* scale, const fl
 int sp_conv3x3_c64(const float* x, int64_t ldx, const float* wt, const float* scale, const float* shift, float* y,
                    int64_t ldy, int n, int h, int w, int act, void* stream);
 /* The same conv on bf16 rows (the bf16 variant): bf16 [64][3][3][64] weights, rows ldx (% 8) / ldy (% 4)
- * elements apart, fp32 accumulate, BN + act in fp32, RNE at the store. */
+ * elements apart, fp32 accumulate, BN (+ the optional pre-activation residual res, bf16 rows ldr apart: the
+ * basic block's shortcut, RN:170-200) + act in fp32, RNE at the store. */
 int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_t* w16, const float* scale, const float* shift,
-                        uint16_t* y, int64_t ldy, int n, int h, int w, int act, void* stream);
+                        uint16_t* y, int64_t ldy, const uint16_t* res, int64_t ldr, int n, int h, int w, int act,
+                        void* stream);
 /* nn.MaxPool2d(3, 2, 1) on NHWC (RN:88). y rows are ldy floats apart (ldy >= c, ldy % 4 == 0), so the
  * result can land in a channel slice of a wider buffer (the fused bottleneck shortcut, ABI v6). */
 int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int h, int w, int c, void* stream);

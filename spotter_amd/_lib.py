@@ -86,7 +86,7 @@ _SIGS = {
     "sp_conv3x3_c32_bf16": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_conv3x3_c32": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_conv3x3_c64": (i32, [vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
-    "sp_conv3x3_c64_bf16": (i32, [vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
+    "sp_conv3x3_c64_bf16": (i32, [vp, i64, vp, vp, vp, vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_upsample2x_nearest": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_layernorm": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),
     "sp_attention": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),

@@ -649,7 +649,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
                                                                   const float* __restrict__ scale,
                                                                   const float* __restrict__ shift,
                                                                   uint16_t* __restrict__ y, int64_t ldx,
-                                                                  int64_t ldy, int nimg, int h, int w, int tiles_x,
+                                                                  int64_t ldy, const uint16_t* __restrict__ res,
+                                                                  int64_t ldr, int nimg, int h, int w, int tiles_x,
                                                                   int tiles_y, int act) {
   __shared__ uint4 lds[B6_HALO + B6_WCH];
   __shared__ float aff[128];
@@ -743,16 +744,26 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
       for (int j = 0; j < 2; ++j) {
         const int ox = ox0 + j * 32 + r;
         if (ox >= w) continue;
-        uint16_t* yrow = y + (((int64_t)b * h + oy) * w + ox) * ldy;
+        const int64_t pix = ((int64_t)b * h + oy) * w + ox;
+        uint16_t* yrow = y + pix * ldy;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int n0 = i * 32 + 8 * g + 4 * hh;
+            float rv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (res) {  // pre-activation residual (the basic block's shortcut), bf16 rows
+              const uint2 q = *reinterpret_cast<const uint2*>(res + pix * ldr + n0);
+              rv[0] = __uint_as_float(q.x << 16);
+              rv[1] = __uint_as_float(q.x & 0xffff0000u);
+              rv[2] = __uint_as_float(q.y << 16);
+              rv[3] = __uint_as_float(q.y & 0xffff0000u);
+            }
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
+              float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
+              if (res) u += rv[e];
               v[e] = act ? fmaxf(u, 0.f) : u;
             }
             *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
@@ -766,17 +777,18 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
 }  // namespace sp
 
 extern "C" int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_t* w16, const float* scale,
-                                   const float* shift, uint16_t* y, int64_t ldy, int n, int h, int w, int act,
-                                   void* stream) {
+                                   const float* shift, uint16_t* y, int64_t ldy, const uint16_t* res, int64_t ldr,
+                                   int n, int h, int w, int act, void* stream) {
   using namespace sp;
   SP_ARG_CHECK(x && w16 && scale && shift && y && n > 0 && h > 0 && w > 0 && (act == 0 || act == 1) &&
                    ldx >= 64 && ldy >= 64 && ldx % 8 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
-                   ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 7) == 0,
-               "sp_conv3x3_c64_bf16: bad args (act none/relu, aligned bf16 rows, ldx % 8, ldy % 4, ld >= 64)");
+                   ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 7) == 0 &&
+                   (!res || (ldr >= 64 && ldr % 4 == 0 && ((uintptr_t)res & 7) == 0)),
+               "sp_conv3x3_c64_bf16: bad args (act none/relu, aligned bf16 rows, ldx % 8, ldy / ldr % 4, ld >= 64)");
   const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + B6_TH - 1) / B6_TH;
   const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
   const unsigned grid = (unsigned)(tiles < g_num_cus ? tiles : g_num_cus);  // persistent: one per CU
   hipLaunchKernelGGL(conv3x3_c64_bf16_kernel, dim3(grid), dim3(512), 0, as_stream(stream), x, w16, scale, shift, y,
-                     ldx, ldy, n, h, w, tiles_x, tiles_y, act);
+                     ldx, ldy, res, ldr, n, h, w, tiles_x, tiles_y, act);
   return check_launch("sp_conv3x3_c64_bf16");
 }

@@ -449,13 +449,14 @@ class Engine:
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):
         pad = cw.k // 2
-        if (cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw and res1 is None
-                and res2 is None and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
-            if self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16":
+        if (cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw and res2 is None
+                and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
+            if (self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16"
+                    and (res1 is None or res1.is_bf16)):
                 # the bf16 variant's stage-0 3x3: direct LDS-halo kernel, bit-identical to the implicit GEMM and
                 # 1.53x it at bs32 / bs256 (814 TF at C3; profiles/r3/bf16/ab_conv3x3_c64_bf16.jsonl)
-                return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act)
-            if self.direct_c64 and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32"):
+                return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act, res1=res1)
+            if self.direct_c64 and res1 is None and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32"):
                 # the fp32 modes' form (sp_conv3x3_c64): slower than the split GEMM today, off by default
                 return ops.conv3x3_c64(x, cw.w, cw.scale, cw.shift, out, n, h, w, act=act)
         if cw.wino is not None and stride == 1 and not kw and not x.is_bf16 and self._wino_pays(n * h * w, cw.cin):

@@ -374,7 +374,7 @@ def conv3x3_c64(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor
 
 
 def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int,
-                     w: int, act=None):
+                     w: int, act=None, res1: V | None = None):
     """The stage-0 3×3 of the bf16 variant (Cin 64 → 64) on bf16 rows (channel-slice views allowed): the direct
     LDS-halo kernel sp_conv3x3_c64_bf16."""
     if not (x.is_bf16 and y.is_bf16) or x.ld % 8 or x.off % 8 or y.ld % 4 or y.off % 4:
@@ -384,9 +384,14 @@ def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.
     m = n * h * w
     xp = x.need(m, 64, "c64b.x", bf16=True)
     yp = y.need(m, 64, "c64b.y", bf16=True)
+    rp, ldr = None, 0
+    if res1 is not None:
+        if not res1.is_bf16 or res1.ld % 4 or res1.off % 4:
+            raise ValueError("conv3x3_c64_bf16: the residual must be 8-byte aligned bf16 rows")
+        rp, ldr = res1.need(m, 64, "c64b.res", bf16=True), res1.ld
     _launch("conv", "sp_conv3x3_c64_bf16", (xp, x.ld, w16.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, y.ld,
-                                            n, h, w, ACT[act], stream()),
-            2 * m * 64 * 576, 2 * (m * 64 + 64 * 576 + m * 64), (m, 64, 576, 3, 1, "bf16-direct"))
+                                            rp, ldr, n, h, w, ACT[act], stream()),
+            2 * m * 64 * 576, 2 * (m * 64 + 64 * 576 + m * 64 * (2 if rp else 1)), (m, 64, 576, 3, 1, "bf16-direct"))
 
 
 def _pool_out(y, m: int, c: int, what: str):

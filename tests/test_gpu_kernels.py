@@ -539,9 +539,10 @@ def test_conv3x3_c64_f32_direct(dev, act, hw, lds):
     assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, 64)).max() <= tol
 
 
-@pytest.mark.parametrize("act,hw,lds", [("relu", (13, 70), (64, 64)), (None, (9, 129), (128, 192)),
-                                        ("relu", (1, 1), (64, 128)), ("relu", (40, 64), (64, 64))])
-def test_conv3x3_c64_bf16_direct(dev, act, hw, lds):
+@pytest.mark.parametrize("act,hw,lds,res", [("relu", (13, 70), (64, 64), False), (None, (9, 129), (128, 192), False),
+                                            ("relu", (1, 1), (64, 128), False), ("relu", (40, 64), (64, 64), False),
+                                            ("relu", (13, 70), (64, 128), True), (None, (9, 129), (128, 64), True)])
+def test_conv3x3_c64_bf16_direct(dev, act, hw, lds, res):
     """sp_conv3x3_c64_bf16 (the bf16 variant's stage-0 3×3) equals the implicit-GEMM bf16 path on the same
     bf16 rows bit for bit (both sum the 576-deep k in (tap, 16-channel) order with v_mfma_f32_32x32x16_bf16
     blocks); channel-slice input / output rows, ragged tiles, one-pixel maps; columns around the slice kept."""
@@ -560,13 +561,20 @@ def test_conv3x3_c64_bf16_direct(dev, act, hw, lds):
     sc, sh = T(rng.uniform(0.5, 1.5, 64).astype(np.float32), dev), T(rng.standard_normal(64).astype(np.float32), dev)
     xv = V(T(xrows.reshape(-1), dev), ldx - 64, ldx)
     ref = torch.full((m * 64,), -1, dtype=torch.int16, device=dev)
+    rv = None
+    if res:  # the basic block's pre-activation shortcut, bf16 rows in a wider buffer
+        r16, _ = _bf16_rows(rng.standard_normal((m, 64)).astype(np.float32))
+        rrows = np.zeros((m, 128), np.int16)
+        rrows[:, 32:96] = r16.reshape(m, 64)
+        rv = V(T(rrows.reshape(-1), dev), 32, 128)
     ops.force_conv_config("14")
     try:
-        ops.conv2d(xv, n, h, w, 64, T(wt, dev), 64, 3, 1, 1, V(ref, 0, 64), scale=sc, shift=sh, act=act, wt16=w16)
+        ops.conv2d(xv, n, h, w, 64, T(wt, dev), 64, 3, 1, 1, V(ref, 0, 64), scale=sc, shift=sh, act=act, wt16=w16,
+                   res1=rv)
     finally:
         ops.force_conv_config(None)
     out = torch.full((m * ldy,), -1, dtype=torch.int16, device=dev)
-    ops.conv3x3_c64_bf16(xv, w16, sc, sh, V(out, ldy - 64, ldy), n, h, w, act=act)
+    ops.conv3x3_c64_bf16(xv, w16, sc, sh, V(out, ldy - 64, ldy), n, h, w, act=act, res1=rv)
     rows = out.cpu().numpy().reshape(m, ldy)
     assert np.all(rows[:, :ldy - 64] == -1)
     assert np.array_equal(rows[:, ldy - 64:], ref.cpu().numpy().reshape(m, 64))
