@@ -70,8 +70,29 @@ def parse():
     ap.add_argument("--microbatches", type=int, default=None,
                     help="concurrent per-GPU batch slices on separate streams (2 overlaps GEMM tails, "
                          "but then per-launch durations overlap)")
+    ap.add_argument("--stream", default="same", choices=["same", "mixed"],
+                    help="same: every source image is --size² (the 640² headline); mixed: the C5 stream, "
+                         "sources cycling through MIXED_SOURCES (SURVEY.md §8 D1.3), resized on the GPU to "
+                         "--size² inside the timed step, target sizes = the source sizes")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds the gloo rendezvous / barrier waits for a missing rank")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU launcher test
+    ap.add_argument("--stub-fail-rank", type=int, default=None, help=argparse.SUPPRESS)  # CPU launcher test
     return ap.parse_args()
+
+
+# the C5 mixed-resolution stream: source (h, w) sizes cycled image by image
+MIXED_SOURCES = [(480, 640), (717, 1200), (720, 1280), (1080, 1920), (1280, 1280), (2160, 3840)]
+
+
+def stream_plan(n_sources: int, batch: int):
+    """Image pool size and, per step of one period, the pool indices of its batch: the stream cycles the
+    sources image by image (image j of the stream is source j mod n_sources), so the pool holds
+    lcm(n_sources, batch) images and the step pattern repeats every pool // batch steps."""
+    import math
+
+    pool = n_sources * batch // math.gcd(n_sources, batch)
+    return pool, [[(k * batch + i) % pool for i in range(batch)] for k in range(pool // batch)]
 
 
 # kernel class -> (bound, peak, unit); peaks from MI355X_MICROARCH.md (dense, no sparsity)
@@ -188,7 +209,8 @@ def load_traffic(args, avg_alg_bytes, key="conv"):
         return None, None
     with open(path) as f:
         t = json.load(f)
-    cfg_key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.mb_eff}"
+    cfg_key = f"{args.preset}_{args.size}_bs{args.batch}_{args.precision}_mb{args.mb_eff}" + (
+        "_mixed" if getattr(args, "stream", "same") == "mixed" else "")
     e = (t.get(cfg_key) or {}).get("classes", {}).get(key)
     if not e:
         return None, None
@@ -290,17 +312,29 @@ def launch_replicas(args) -> int:
                    CUDA_VISIBLE_DEVICES=dev, SPOTTER_REPLICA_DEVICE="0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
                                       stdout=None if i == 0 else sys.stderr))
-    rc = 0
+    # poll every child: the first non-zero exit (any rank) kills the others at once, instead of rank 0
+    # sitting in the gloo rendezvous / barrier until its timeout
+    rc, failed = 0, None
     try:
-        for p in procs:
-            rc = max(rc, p.wait())
-            if rc:
+        live = list(range(n))
+        while live:
+            for i in list(live):
+                code = procs[i].poll()
+                if code is None:
+                    continue
+                live.remove(i)
+                if code != 0 and failed is None:
+                    rc, failed = code, i
+            if failed is not None:
                 break
+            time.sleep(0.05)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+    if failed is not None:
+        print(f"bench.py: replica rank {failed} exited with {rc}; stopped the other ranks", file=sys.stderr)
     return rc
 
 
@@ -415,18 +449,32 @@ def make_step(args, rank, local):
     args.mb_eff = eng.micro_batches_for(args.batch)
     eng.stagger = args.stagger
     B, S = args.batch, args.size
-    imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
-    imgs = [torch.from_numpy(im).to(dev) for im in imgs_host]  # resident in HBM
-    px = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
     K = cfg.num_queries
-    tsz = torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev)
+    if args.stream == "mixed":
+        # C5: a pool of uint8 sources of the stream's sizes, resident in HBM; each step takes the next B of
+        # the cycle (different sizes in one batch, resized on the GPU), post-processed at its source sizes
+        from spotter_amd.synthetic import synthetic_image
+
+        npool, plan = stream_plan(len(MIXED_SOURCES), B)
+        pool = [torch.from_numpy(synthetic_image(1234 + 1000 * rank + j, *MIXED_SOURCES[j % len(MIXED_SOURCES)]))
+                .to(dev) for j in range(npool)]
+        batches = [([pool[j] for j in idx], torch.tensor([list(pool[j].shape[:2]) for j in idx], dtype=torch.int32,
+                                                          device=dev)) for idx in plan]
+    else:
+        imgs_host = synthetic_batch(B, S, S, seed0=1234 + 1000 * rank)
+        batches = [([torch.from_numpy(im).to(dev) for im in imgs_host],  # resident in HBM
+                    torch.tensor([[S, S]] * B, dtype=torch.int32, device=dev))]
+    px = torch.empty((B, 3, S, S), dtype=torch.float32, device=dev)
     scores = torch.empty((B, K), device=dev)
     labels = torch.empty((B, K), dtype=torch.int64, device=dev)
     boxes = torch.empty((B, K, 4), device=dev)
     counts = torch.empty((B,), dtype=torch.int32, device=dev)
     work = torch.empty((B, K), dtype=torch.int32, device=dev)
+    it = [0]
 
     def step():
+        imgs, tsz = batches[it[0] % len(batches)]
+        it[0] += 1
         ops.preprocess_u8(imgs, px, S, S)
         logits, pred = eng.forward(px)
         ops.postprocess(logits, pred, tsz, K, 0.5, scores, labels, boxes, counts, work)
@@ -445,11 +493,16 @@ def main():
     if args.gpus > 1 and world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
+    if args.stub_fail_rank is not None and rank == args.stub_fail_rank:
+        return 3  # CPU launcher test: this replica dies before the rendezvous
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")
+        import datetime
+
+        # a rank that never arrives ends the run in minutes, not gloo's 30-minute default
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
     from spotter_amd.replicas import all_gather_obj, barrier, max_over_ranks
 
     step, sync, set_hook = make_step(args, rank, local)
@@ -514,6 +567,10 @@ def main():
             classes[kind] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                              "frac": round(ach / peak, 4), "ms_per_step": round(c["busy"] / args.steps, 3),
                              "launches_per_step": c["n"] // args.steps}
+            tr, tnote = load_traffic(args, c["bytes"] / max(1, c["n"]), key=kind)
+            if tr is not None:  # PMC HBM bytes per launch of this class, when collected on this config
+                classes[kind]["traffic"] = tr
+                classes[kind]["traffic_source"] = tnote
             if c.get("gather"):
                 classes[kind]["l2_gather"] = {
                     "achieved": round(c["gather"] / 1e9 / (c["busy"] * 1e-3), 1), "unit": "GB/s",
@@ -553,14 +610,21 @@ def main():
 
     if rank == 0:
         S = args.size
+        mixed = args.stream == "mixed"
+        workload = f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess"
+        if mixed:
+            workload = (f"RT-DETRv2-{args.preset} mixed-resolution stream (sources cycling "
+                        f"{', '.join(f'{h}x{w}' for h, w in MIXED_SOURCES)}, uint8 resident in HBM) resized on the "
+                        f"GPU to {S}x{S} inside the step, batch={B}/GPU preprocess+forward+postprocess")
         line = {
-            "metric": (BASELINE_METRIC if (args.preset, S, B, args.precision) == ("r101vd", 640, 32, "fp32")
-                       else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B} {args.precision}"),
+            "metric": (BASELINE_METRIC if (args.preset, S, B, args.precision, mixed) == ("r101vd", 640, 32, "fp32", False)
+                       else f"images/sec RT-DETRv2-{args.preset} {S}² bs{B} {args.precision}"
+                       + (" mixed-resolution stream" if mixed else "")),
             "value": round(value, 2), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic uint8 RGB images (seeded), synthetic deterministic weights",
-            "config": {"workload": f"RT-DETRv2-{args.preset} {S}x{S} batch={B}/GPU preprocess+forward+postprocess",
+            "config": {"workload": workload, **({"stream_sources_hw": MIXED_SOURCES} if mixed else {}),
                        "model": f"rtdetr_v2_{args.preset}", "global_batch": B * world, "image_size": S,
                        "parallelism": f"replicas x{world}"},
             "per_rank": per_rank,

@@ -90,6 +90,7 @@ class MicroBatcher:
             items = self._take()
             if items is None:
                 return
+            outs, err = None, None
             try:
                 xs = [x.to(self.device, non_blocking=True) for x, _ in items]
                 x = xs[0] if len(xs) == 1 else torch.cat(xs, 0)
@@ -100,20 +101,25 @@ class MicroBatcher:
                 outs = []
                 for (xi, fut) in items:
                     k = xi.shape[0]
-                    outs.append((fut, logits[off:off + k].clone(), boxes[off:off + k].clone()))
+                    outs.append((logits[off:off + k].clone(), boxes[off:off + k].clone()))
                     off += k
                 if self.device.type == "cuda":
                     torch.cuda.current_stream().synchronize()
-                with self._pending_lock:
-                    self._pending -= len(items)
-                for fut, lg, bx in outs:
-                    fut.set_result((lg, bx))
             except BaseException as e:  # every waiting caller sees the failure
+                err = e
+            finally:
                 with self._pending_lock:
-                    self._pending -= sum(1 for _, f in items if not f.done())
-                for _, fut in items:
-                    if not fut.done():
-                        fut.set_exception(e)
+                    self._pending -= len(items)  # once per item, whatever happened
+            for i, (_, fut) in enumerate(items):
+                # each future on its own: a caller that cancelled its future (or one already resolved)
+                # cannot fail the others or the collector thread
+                try:
+                    if err is not None:
+                        fut.set_exception(err)
+                    else:
+                        fut.set_result(outs[i])
+                except Exception:
+                    pass
 
     def close(self):
         self._q.put(None)

@@ -205,6 +205,10 @@ def resolve_pretrained(name_or_path: str, revision: str = "main", need: str = "c
     as revision). Raises OSError naming the searched paths when no snapshot holding `need` exists:
     there is no network and no silent substitute."""
     if os.path.isdir(name_or_path):
+        if need and not os.path.isfile(os.path.join(name_or_path, need)):
+            # an existing but empty directory (e.g. an image built without its checkpoint context) is
+            # not a checkpoint: refuse here rather than fail later in every replica
+            raise OSError(f"{name_or_path!r} is a directory without {need}: not a checkpoint")
         return name_or_path
     repo = name_or_path.strip("/")
     if repo.count("/") > 1 or not repo:
@@ -229,19 +233,32 @@ def resolve_pretrained(name_or_path: str, revision: str = "main", need: str = "c
                   f"download.py does, or pass a checkpoint directory)")
 
 
-def load_local(path: str):
+# Unknown keys named like RTDetrV2Config model fields (configuration_rt_detr_v2.py:136-189 uses these
+# prefixes for every architecture field): a later transformers version adding one would change the
+# arithmetic, so it is refused rather than ignored.
+_MODEL_FIELD_PREFIXES = ("encoder", "decoder", "backbone", "anchor", "num_", "d_model", "feat_", "with_", "layer_")
+
+
+def check_fields(js: dict, strict: bool = False) -> None:
+    """Refuse unknown config.json keys that look like model fields (always) or any unknown key
+    (strict=True, what the image build uses); other unknown keys only warn."""
+    unk = unknown_fields(js)
+    model_like = [k for k in unk if k.startswith(_MODEL_FIELD_PREFIXES)]
+    if model_like or (strict and unk):
+        raise UnsupportedConfig(f"config.json fields this loader does not implement: {model_like or unk}")
+    if unk:
+        import warnings
+
+        warnings.warn(f"config.json fields this loader does not read (assumed not to change inference): {unk}",
+                      stacklevel=3)
+
+
+def load_local(path: str, strict: bool = False):
     from safetensors.numpy import load_file
 
     with open(os.path.join(path, "config.json")) as f:
         js = json.load(f)
-    unk = unknown_fields(js)
-    if unk:
-        # not an inference field this loader knows: the _FIXED and activation fields are refused
-        # hard by config_from_hf; anything else is reported, not fatal
-        import warnings
-
-        warnings.warn(f"config.json fields this loader does not read (assumed not to change inference): {unk}",
-                      stacklevel=2)
+    check_fields(js, strict)
     cfg = config_from_hf(js)
     raw = {}
     for fn in sorted(os.listdir(path)):
@@ -285,3 +302,25 @@ def save_local(path: str, cfg: SpotterConfig, weights: dict) -> None:
         json.dump(hf_config_dict(cfg), f, indent=1)
     save_file({v4_key(k): np.ascontiguousarray(v, dtype=np.float32) for k, v in weights.items()},
               os.path.join(path, "model.safetensors"))
+
+
+def check_image_model(name: str) -> str:
+    """What the image build runs on its ENV MODEL_NAME (deploy/Dockerfile.rocm): a synthetic: name is
+    accepted as is; anything else must resolve to a directory holding config.json whose every field
+    the loader implements (strict). Returns the resolved directory; raises otherwise."""
+    if name.startswith("synthetic:"):
+        return name
+    d = resolve_pretrained(name)
+    with open(os.path.join(d, "config.json")) as f:
+        js = json.load(f)
+    check_fields(js, strict=True)
+    config_from_hf(js)
+    return d
+
+
+if __name__ == "__main__":
+    import sys
+
+    if len(sys.argv) != 3 or sys.argv[1] != "--check":
+        sys.exit("usage: python -m spotter_amd.checkpoint --check <MODEL_NAME>")
+    print("weights:", check_image_model(sys.argv[2]))

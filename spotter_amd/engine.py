@@ -165,6 +165,9 @@ class Engine:
         # 42 TF/s (2.47 ms/step) against 1.4 ms/step for the unfused GEMMs + 21 sp_layernorm launches
         # (profiles/r2/fused_ln_ab.json); it stays selectable and tested.
         self.fuse_ln = fuse_ln
+        if fuse_ln and PRECISIONS.get(precision, ("", ""))[1] == "bf16":
+            # the fused-LN tile runs fp32 weights: it would silently raise the bf16 linears' operand precision
+            raise ValueError(f"fuse_ln=True runs the linears on fp32 weights: not available with precision={precision!r}")
         # stride-1 3x3 convs as Winograd F(m x m, 3x3) on the split GEMM (sp_winograd_f{2,4}3_*): "auto"
         # (default) = those on the split operand mode with Cin >= 128 for F(4x4) (1.4-2.6x faster than the
         # implicit GEMM at bs32, profiles/r2/tune_wino_f43_x3.json) or Cin >= 256 for F(2x2) (1.25-1.8x,

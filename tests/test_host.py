@@ -158,6 +158,26 @@ def test_bench_launcher_spawns_one_replica_per_gpu():
     assert 2 * 32 / 0.040 < line["value"] <= 2 * 32 / 0.020 * 1.01
 
 
+@pytest.mark.parametrize("fail_rank", [1, 0])
+def test_bench_launcher_fails_fast_when_a_replica_dies(fail_rank):
+    """One replica exits 3 before the rendezvous: the launcher reports that code within seconds and
+    kills the other rank, which would otherwise wait in the gloo rendezvous until its timeout."""
+    import sys
+    import time
+
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        env.pop(v, None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--stub-step-ms", "20", "--stub-fail-rank", str(fail_rank)],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert f"replica rank {fail_rank} exited with 3" in r.stderr
+    assert time.time() - t0 < 60
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
 @pytest.mark.parametrize("preset", ["r18vd", "r101vd"])
 def test_config_from_hf_reads_hf_config_json(preset, tmp_path):
     """config.json as HF itself writes it (RTDetrV2Config.save_pretrained) → the same SpotterConfig as the
@@ -324,6 +344,14 @@ def test_loader_skips_bookkeeping_keys_and_warns_on_unknown(tmp_path):
     with pytest.warns(UserWarning, match="some_future_field"):
         cfg, w = load_local(str(tmp_path))
     assert cfg.depths == PRESETS["r18vd"].depths and w == {}
+    from spotter_amd.checkpoint import UnsupportedConfig
+
+    with pytest.raises(UnsupportedConfig, match="some_future_field"):
+        load_local(str(tmp_path), strict=True)  # what the image build check uses
+    js["decoder_future_gate"] = True  # named like a model field: refused even when not strict
+    (tmp_path / "config.json").write_text(json.dumps(js))
+    with pytest.raises(UnsupportedConfig, match="decoder_future_gate"):
+        load_local(str(tmp_path))
 
 
 @pytest.mark.parametrize("wm", [2, 4])
@@ -423,7 +451,74 @@ def test_rayservice_template_renders():
     assert worker["resources"]["requests"]["amd.com/gpu"] == gpus
     assert int(wg["rayStartParams"]["num-gpus"]) == gpus == dep["num_replicas"] == 8
     env = {e["name"]: e["value"] for e in worker["env"]}
-    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["MODEL_NAME"].startswith("/models/")
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    # as the reference template (configs/rayservice-template.yaml:41-59): no pod overrides MODEL_NAME,
+    # the image's ENV decides for head and workers alike
+    assert "MODEL_NAME" not in env and "MODEL_NAME" not in {e["name"] for e in head.get("env", [])}
+
+
+def _dockerfile_recipe():
+    """(ARG MODEL_NAME default, the directory the checkpoint context is copied to) from deploy/Dockerfile.rocm."""
+    text = open(os.path.join(ROOT, "deploy", "Dockerfile.rocm")).read()
+    default = re.search(r'^ARG MODEL_NAME="([^"]*)"', text, re.M).group(1)
+    ckpt_dir = re.search(r"^COPY --from=checkpoint / (\S+)", text, re.M).group(1).rstrip("/")
+    assert "python -m spotter_amd.checkpoint --check \"$MODEL_NAME\"" in text
+    return default, ckpt_dir
+
+
+def _pod_model_names(image_env):
+    """MODEL_NAME each container of the rendered template sees: its own env entry, else the image ENV."""
+    import yaml
+
+    src = open(os.path.join(ROOT, "deploy", "rayservice-template.yaml")).read()
+    body = "\n".join(l for l in src.splitlines() if not l.lstrip().startswith("#"))
+    rc = yaml.safe_load(body.replace("{{.DockerImage}}", "img"))["spec"]["rayClusterConfig"]
+    conts = list(rc["headGroupSpec"]["template"]["spec"]["containers"])
+    for wg in rc["workerGroupSpecs"]:
+        conts += wg["template"]["spec"]["containers"]
+    return {c["name"]: {e["name"]: e["value"] for e in c.get("env", [])}.get("MODEL_NAME", image_env) for c in conts}
+
+
+def test_every_pod_model_name_resolves_for_each_build_recipe(tmp_path, monkeypatch):
+    """The two documented image recipes of deploy/Dockerfile.rocm, replayed on a scratch filesystem:
+    (1) the default hub name, pre-fetched into the HF cache by spotter_download (the checkpoint
+    directory stays empty), (2) --build-context checkpoint=<dir> --build-arg MODEL_NAME=<that dir>.
+    For each, the MODEL_NAME every pod of the rendered template sees resolves to a directory holding
+    config.json, and the image's build check accepts it. The broken mix (MODEL_NAME = the checkpoint
+    directory without the checkpoint context) is refused by the build check instead of by every replica."""
+    from spotter_amd import checkpoint
+    from spotter_amd.config import PRESETS
+    from spotter_amd.weights import generate
+
+    default, ckpt_dir = _dockerfile_recipe()
+    cfg = PRESETS["r18vd"]
+    w = generate(cfg, seed=1)
+    for var in ("HF_HUB_CACHE", "HUGGINGFACE_HUB_CACHE", "TRANSFORMERS_CACHE"):
+        monkeypatch.delenv(var, raising=False)
+    root = tmp_path / "img"
+    baked = root / ckpt_dir.lstrip("/")
+
+    def check(image_env):
+        names = _pod_model_names(image_env)
+        assert len(names) >= 2 and set(names.values()) == {image_env}, names
+        for n in names.values():
+            local = str(root / n.lstrip("/")) if n.startswith("/") else n
+            d = checkpoint.resolve_pretrained(local)
+            assert os.path.isfile(os.path.join(d, "config.json"))
+            assert checkpoint.check_image_model(local) == d
+
+    # recipe 1: hub name, snapshot in the image's HF cache, /models/... empty
+    monkeypatch.setenv("HF_HOME", str(root / "hf"))
+    _fake_hub_cache(root / "hf" / "hub", default, cfg, w)
+    baked.mkdir(parents=True)
+    check(default)
+    # the broken mix: MODEL_NAME = the (empty) checkpoint directory → refused at build time
+    with pytest.raises(OSError, match="without config.json"):
+        checkpoint.check_image_model(str(baked))
+    # recipe 2: the checkpoint context baked into ckpt_dir, MODEL_NAME = that directory
+    monkeypatch.setenv("HF_HOME", str(tmp_path / "empty_hf"))
+    checkpoint.save_local(str(baked), cfg, w)
+    check(ckpt_dir)
 
 
 def test_dockerfile_copies_exist_in_their_contexts():
@@ -580,6 +675,35 @@ def test_microbatcher_coalesces_concurrent_calls():
     mb2.close()
 
 
+def test_microbatcher_cancelled_caller_does_not_fail_the_others():
+    """A caller that cancels its Future while its batch runs: the other callers of that batch still get
+    their rows, the pending count returns to zero (so coalescing stays on), the collector survives."""
+    import threading
+    import time
+
+    import torch
+
+    from spotter_amd.batching import MicroBatcher
+
+    gate = threading.Event()
+
+    def run(x):
+        gate.wait(5)
+        return x[:, 0, 0, :1].unsqueeze(-1), x[:, 0, :1, :4]
+
+    mb = MicroBatcher(run, "cpu", max_batch=8, max_wait_ms=100)
+    futs = [mb.submit(torch.full((1, 3, 4, 4), float(i))) for i in range(3)]
+    time.sleep(0.2)  # all three taken into one batch, blocked in run
+    assert futs[1].cancel()
+    gate.set()
+    assert float(futs[0].result(5)[0].flatten()[0]) == 0.0 and float(futs[2].result(5)[0].flatten()[0]) == 2.0
+    assert futs[1].cancelled()
+    time.sleep(0.05)
+    assert mb._pending == 0
+    assert float(mb(torch.full((1, 3, 4, 4), 7.0))[0].flatten()[0]) == 7.0  # the collector is alive
+    mb.close()
+
+
 def test_microbatcher_lone_serial_caller_is_not_delayed():
     """The unchanged serve.py calls the model once per image, serially: with nobody else pending the
     batcher dispatches at once instead of waiting max_wait_ms for company."""
@@ -658,3 +782,15 @@ def test_coco_ap_hand_built_cases():
     many = {"boxes": np.array([[100, 100, 110, 110]] * 100 + [[0, 0, 10, 10]], float),
             "labels": np.ones(101, int), "scores": np.concatenate([np.full(100, 0.9), [0.1]])}
     assert ap([many], [{"boxes": one["boxes"], "labels": np.array([1])}])["map"] == 0.0
+
+
+def test_engine_refuses_fused_layernorm_on_bf16_linears():
+    """fuse_ln runs the linears on fp32 weights: with bf16 linears ("bf16", and its round-2 alias
+    "bf16-all") that would change the operand precision silently, so the Engine refuses at construction
+    (before any device call), not at the first forward."""
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+
+    for prec in ("bf16", "bf16-all"):
+        with pytest.raises(ValueError, match="fuse_ln"):
+            Engine(PRESETS["r18vd"], {}, "cpu", precision=prec, fuse_ln=True)

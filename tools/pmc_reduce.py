@@ -16,8 +16,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce", "stem_conv")), ("msda", ("msda",)), ("attention", ("attn_",)),
-           ("preprocess", ("preprocess_kernel",)), ("topk", ("topk",)), ("layernorm", ("layernorm",))]
+CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce", "stem_conv", "conv3x3")), ("msda", ("msda",)), ("attention", ("attn_",)),
+           ("preprocess", ("preprocess",)), ("topk", ("topk",)), ("layernorm", ("layernorm",))]
 LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_", "preprocess": None, "topk": "topk",
            "layernorm": "layernorm"}
 
@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--precision", default="fp32")
     ap.add_argument("--microbatches", type=int, default=None)
+    ap.add_argument("--stream", default="same")
     a, _ = ap.parse_known_args()
     if a.microbatches is None:  # the engine's default split (Engine.micro_batches_for)
         a.microbatches = 1
@@ -86,7 +87,7 @@ def main():
         write_b = wr[cls]["kib"] * 1024 / max(1, wr[cls]["n"])
         res[cls] = {"hbm_bytes_per_launch": int(fetch_b + write_b), "fetch_bytes_per_launch_x2": int(fetch_b),
                     "write_bytes_per_launch": int(write_b), "launches": n}
-    key = f"{a.preset}_{a.size}_bs{a.batch}_{a.precision}_mb{a.microbatches}"
+    key = f"{a.preset}_{a.size}_bs{a.batch}_{a.precision}_mb{a.microbatches}" + ("_mixed" if a.stream == "mixed" else "")
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     allr = json.load(open(path)) if os.path.exists(path) else {}
     allr[key] = {"conv_hbm_bytes_per_launch": res.get("conv", {}).get("hbm_bytes_per_launch"), "classes": res,
