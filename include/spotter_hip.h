@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 10
+#define SP_ABI_VERSION 11
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -113,6 +113,13 @@ typedef struct {
   uint16_t* C_bf16;
   const uint16_t* res1_bf16;
   const uint16_t* res2_bf16;
+  /* ABI v11: in-kernel split-K combine. With a workspace and split-K, splitk_flags (non-NULL) is an array of
+   * splitk_flags_len int32 arrival counters that must be ZERO before the call and are zero again when the
+   * launch completes (the same array can serve every sp_conv2d call of one stream): the last workgroup of
+   * each output tile to finish adds the partial sums in fixed z order (bit-identical to the separate reduce
+   * launch used when splitk_flags is NULL or shorter than the tile grid) and applies the epilogue. */
+  int32_t* splitk_flags;
+  int64_t splitk_flags_len;
 } sp_conv_desc;
 
 /*
@@ -154,6 +161,8 @@ int sp_conv2d(const sp_conv_desc* d, void* stream);
  * the CALLING THREAD (-1, the default, = chosen by shape). Nothing on the product path calls it, and
  * no environment variable is read: the production tile choice cannot be changed from outside. */
 int sp_set_conv_config(int cfg);
+/* The same override for split-K launches only (ABI v11; -1 = the library's choice): bs1 tile tuning. */
+int sp_set_splitk_config(int cfg);
 
 /* 3x3 stride-1 pad-1 convolution by Winograd F(2x2, 3x3) (ABI v9): the same result contract as
  * sp_conv2d on the same descriptor (KH = KW = 3, stride 1, pad 1; act, scale / shift, res1 / res2 as

@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -44,6 +44,7 @@ class SpConvDesc(C.Structure):
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
         ("C_bf16", vp), ("res1_bf16", vp), ("res2_bf16", vp),
+        ("splitk_flags", vp), ("splitk_flags_len", i64),
     ]
 
 
@@ -69,6 +70,7 @@ _SIGS = {
     "sp_preprocess_u8": (i32, [C.POINTER(SpImageU8), i32, i32, i32, vp, vp]),
     "sp_conv2d": (i32, [C.POINTER(SpConvDesc), vp]),
     "sp_set_conv_config": (i32, [i32]),
+    "sp_set_splitk_config": (i32, [i32]),
     "sp_conv3x3_winograd": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
     "sp_winograd_f23_input": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
     "sp_winograd_f23_gemm": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),

@@ -36,6 +36,11 @@ struct ConvArgs {
   // producer instead of split per fragment in the GEMM (lda and bs_a count bf16 elements then).
   const uint16_t* A16 = nullptr;
   int64_t a_plane_stride = 0;
+  // In-kernel split-K combine (ABI v11, sp_conv_desc.splitk_flags): one zeroed arrival counter per
+  // output tile (indexed by the tile's x / y grid position, shared by its z slices); null = the
+  // separate splitk_reduce launch. Launchers clear it when the grid has more tiles than counters.
+  int32_t* flags = nullptr;
+  int64_t flags_len = 0;
 };
 
 // Output row offset (elements): plain row-major (out_rows_per_group == 0) or grouped rows.
@@ -235,6 +240,49 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
       }
     }
   }
+}
+
+// In-kernel split-K combine of output tile `tile` (BM × BN from m0, n0), called by every workgroup of a
+// split-K launch with p.flags set, after all of its threads stored their raw partial sums: the last of the
+// p.splits z slices to arrive (per-tile counter, agent-scope atomic: the slices may run on different XCDs,
+// whose L2s the release / acquire fences write back / invalidate) adds the partial slabs in fixed z order
+// 0, 1, ..., splits-1 — splitk_reduce_kernel's order, so the result is bit-identical to it and does not
+// depend on which slice came last — runs the fused epilogue and re-arms the counter for the next launch on
+// the stream. Replaces the reduce launch (one per split-K GEMM: 135 of a bs1 forward's ≈430 kernels).
+// lds_flag: one int of the kernel's own LDS, free by now.
+template <int NT>
+__device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_t m0, int n0, int BM, int BN,
+                                             int* lds_flag) {
+  __threadfence();  // release: this thread's partial stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(p.flags + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = old == p.splits - 1;
+  }
+  __syncthreads();
+  if (!*lds_flag) return;
+  __threadfence();  // acquire: every slice's partial stores
+  const int n4 = BN / 4;
+  const int64_t zs = p.M * p.ldp;
+  for (int idx = threadIdx.x; idx < BM * n4; idx += NT) {
+    const int row = idx / n4;
+    const int n = n0 + (idx - row * n4) * 4;
+    const int64_t m = m0 + row;
+    if (m >= p.M || n >= p.d.Cout) continue;
+    const float* src = p.partial + m * p.ldp + n;
+    float4 v = *reinterpret_cast<const float4*>(src);
+    for (int z = 1; z < p.splits; ++z) {
+      const float4 u = *reinterpret_cast<const float4*>(src + z * zs);
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    epilogue_store(p, m, n, v);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(p.flags + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Host side: keep the in-kernel combine only when every tile of the grid has its own counter.
+inline void splitk_flags_fit(ConvArgs& a, int64_t tiles) {
+  if (a.splits <= 1 || tiles > a.flags_len) a.flags = nullptr;
 }
 
 // Row-LayerNorm epilogue (sp_conv_desc.ln_gamma): the workgroup holds whole output rows — BM = 32 rows

@@ -283,6 +283,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.splits > 1 && p.flags) {
+    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
+    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+  }
 }
 
 #if SP_X3S_STAMP
@@ -499,6 +503,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.splits > 1 && p.flags) {
+    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
+    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+  }
 }
 
 template <int WM, int WN, int TM, int TN, int NS>
@@ -726,6 +734,10 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.splits > 1 && p.flags) {
+    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
+    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+  }
 }
 
 template <int TM, int TN>
@@ -1340,13 +1352,15 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
+  ConvArgs b = a;
+  splitk_flags_fit(b, tiles);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, b);
   else
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, b);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3)" : "sp_conv2d(bf16)");
-  if (rc || a.splits == 1) return rc;
-  return launch_splitk_reduce(a, s);
+  if (rc || b.splits == 1 || b.flags) return rc;
+  return launch_splitk_reduce(b, s);
 }
 
 }  // namespace
@@ -1383,13 +1397,15 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   if (!a.fast) {  // generic gather: one small-tile instance per operand mode
     const int64_t tiles = ((a.M + 63) / 64) * ((a.d.Cout + 63) / 64);
     dim3 grid((unsigned)tiles, 1, a.splits);
+    ConvArgs b = a;
+    splitk_flags_fit(b, tiles);
     if (planes == 3)
-      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 3, false>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 3, false>), grid, dim3(256), 0, s, b);
     else
-      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 1, false>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 1, false>), grid, dim3(256), 0, s, b);
     int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 generic)" : "sp_conv2d(bf16 generic)");
-    if (rc || a.splits == 1) return rc;
-    return launch_splitk_reduce(a, s);
+    if (rc || b.splits == 1 || b.flags) return rc;
+    return launch_splitk_reduce(b, s);
   }
   if (cfg >= 70 && cfg <= 75 && (a.d.C_bf16 || a.d.res1_bf16 || a.d.res2_bf16)) cfg = -1;  // register epilogues: fp32 rows only
   if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1 && a.vec_epi) {
@@ -1432,11 +1448,11 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
     cfg += 100;
   const int gc = cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;  // cfg + 100: the LDS-DMA residual epilogue variant
-  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
+  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 68)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 68 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

@@ -1,0 +1,75 @@
+"""bs1 forward A/B on hipGraph replays: the split-K combine (in-kernel vs the reduce launch) and the tile of
+the split-K launches (sp_set_splitk_config), same process, variants interleaved over several rounds.
+
+    python tools/bs1_ab.py [--preset r101vd] [--reps 100] [--rounds 3] [--variants reduce:4,inkernel:4,...]
+
+Prints one JSON line per variant: median replay ms per round, and the max |Δ| of its logits / boxes against
+the first variant (bit-identical expected for the same tile; same-order sums for another tile)."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from spotter_amd import ops
+from spotter_amd.config import PRESETS
+from spotter_amd.engine import Engine
+from spotter_amd.graph import GraphRunner
+from spotter_amd.weights import generate
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="r101vd")
+    ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="reduce:4,inkernel:4,inkernel:14,inkernel:66,inkernel:67,inkernel:68")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    cfg = PRESETS[a.preset]
+    dev = torch.device("cuda", 0)
+    eng = Engine(cfg, generate(cfg, seed=0), dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
+    variants = [v.split(":") for v in a.variants.split(",")]
+    runners, ref = {}, None
+    res = {}
+    for mode, c in variants:
+        eng.splitk_inkernel = mode == "inkernel"
+        ops.force_splitk_config(c)
+        try:
+            r = GraphRunner(eng, 1, cfg.image_size, cfg.image_size)
+        finally:
+            ops.force_splitk_config(None)
+        lg, bx = r(x)
+        torch.cuda.synchronize()
+        out = (lg.cpu().numpy().copy(), bx.cpu().numpy().copy())
+        if ref is None:
+            ref = out
+        key = f"{mode}:{c}"
+        runners[key] = r
+        res[key] = {"max_dlogit": float(np.abs(out[0] - ref[0]).max()), "max_dbox": float(np.abs(out[1] - ref[1]).max()),
+                    "bit_identical": bool(np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])), "ms": []}
+    for _ in range(a.rounds):
+        for key, r in runners.items():
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                r.graph.replay()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            res[key]["ms"].append(round(float(np.median(ts)), 4))
+    for key, v in res.items():
+        v["median_ms"] = round(float(np.median(v["ms"])), 4)
+        print(json.dumps({"variant": key, **v}), flush=True)
+    if a.out:
+        json.dump(res, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
