@@ -274,6 +274,41 @@ int sp_postprocess(const float* logits, const float* boxes, const int32_t* targe
                    int q, int c, int k, float threshold, float* scores, int64_t* labels,
                    float* boxes_xyxy, int32_t* counts, int32_t* work, void* stream);
 
+/*
+ * JPEG decode (ABI v11): the step in front of A1 — serve.py:96-97 `Image.open(BytesIO(...)).convert("RGB")`,
+ * which Pillow runs through libjpeg-turbo (ISLOW integer IDCT, fancy upsampling, integer YCbCr→RGB).
+ * Split as the hardware wants it: the Huffman entropy decode (a serial bit stream) on the host, everything
+ * per pixel on the GPU. Supported: 8-bit baseline / extended / progressive Huffman JPEGs with 1 (gray) or 3
+ * (YCbCr, or RGB per the Adobe / component-id rules of libjpeg) components, luma at the maximum sampling
+ * factors and chroma at 1x or 2x below it in each direction, restart intervals. Anything else returns
+ * SP_JPEG_UNSUPPORTED (the caller keeps the reference's host decode for that image).
+ */
+#define SP_JPEG_UNSUPPORTED (-10)
+typedef struct {
+  int32_t width, height;
+  int32_t ncomp;            /* 1 or 3 */
+  int32_t color;            /* 0 gray, 1 YCbCr, 2 RGB */
+  int32_t progressive;
+  int32_t max_h, max_v;     /* maximum sampling factors */
+  int32_t h[3], v[3];       /* sampling factors per component */
+  int32_t bw[3], bh[3];     /* coefficient blocks per row / block rows per component (MCU-padded) */
+  int64_t block_off[3];     /* first block of each component in the coefficient array */
+  int64_t total_blocks;     /* coefficient array: total_blocks * 64 int16, natural (row-major) order */
+  int64_t plane_off[3];     /* byte offset of each component's sample plane (bw*8 x bh*8) in `work` */
+  int64_t plane_bytes;      /* bytes of `work` sp_jpeg_to_rgb needs */
+  uint16_t quant[3][64];    /* dequantisation tables (natural order), latched at each component's first scan */
+} sp_jpeg_layout;
+/* Host: parse the JPEG in data[0:len) into *lay; with coefs != NULL (coef_elems >= total_blocks*64) also run
+ * the entropy decode (jdhuff.c / jdphuff.c semantics, including progressive refinement scans and restart
+ * markers; truncated data decodes as zeros, as libjpeg does) and write the quantised coefficients. No device
+ * call: safe without a GPU. */
+int sp_jpeg_decode_coefs(const uint8_t* data, int64_t len, sp_jpeg_layout* lay, int16_t* coefs, int64_t coef_elems);
+/* Device: coefficients (device copy of the array above) → RGB: dequantise + ISLOW IDCT per 8x8 block into the
+ * component planes in `work`, then fancy upsampling + YCbCr→RGB into rgb (uint8 HWC rows rgb_stride bytes
+ * apart, the exact pixels Pillow's convert("RGB") produces). */
+int sp_jpeg_to_rgb(const int16_t* coefs, const sp_jpeg_layout* lay, uint8_t* work, int64_t work_bytes, uint8_t* rgb,
+                   int64_t rgb_stride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

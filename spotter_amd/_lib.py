@@ -62,6 +62,17 @@ class SpMsdaDesc(C.Structure):
     ]
 
 
+class SpJpegLayout(C.Structure):
+    _fields_ = [
+        ("width", i32), ("height", i32), ("ncomp", i32), ("color", i32), ("progressive", i32),
+        ("max_h", i32), ("max_v", i32), ("h", i32 * 3), ("v", i32 * 3), ("bw", i32 * 3), ("bh", i32 * 3),
+        ("block_off", i64 * 3), ("total_blocks", i64), ("plane_off", i64 * 3), ("plane_bytes", i64),
+        ("quant", (C.c_uint16 * 64) * 3),
+    ]
+
+
+SP_JPEG_UNSUPPORTED = -10
+
 _SIGS = {
     "sp_abi_version": (i32, []),
     "sp_last_error": (C.c_char_p, []),
@@ -99,6 +110,8 @@ _SIGS = {
     "sp_ref_init": (i32, [vp, i64, vp, vp, i32, i32, vp, vp]),
     "sp_box_refine": (i32, [vp, i64, vp, i32, vp]),
     "sp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp]),
+    "sp_jpeg_decode_coefs": (i32, [vp, i64, C.POINTER(SpJpegLayout), vp, i64]),
+    "sp_jpeg_to_rgb": (i32, [vp, C.POINTER(SpJpegLayout), vp, i64, vp, i64, vp]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -43,6 +43,25 @@ struct ConvArgs {
   int64_t flags_len = 0;
 };
 
+// Buffer resource over the split-K partial slabs (wave-uniform: built from kernel arguments only).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t partial_rsrc(const ConvArgs& p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, (int)(p.splits * p.M * p.ldp * 4), 0x00020000);
+}
+
+// Raw partial sums of row m, channels n..n+3 of z slice blockIdx.z. With the in-kernel combine (p.flags) the
+// slab is stored write-through (sc1: the line leaves this XCD's L2 at once), so the last-arriving slice on
+// any XCD reads it with sc1 loads and neither side needs a cache-wide fence (cdna_hip_programming.md §6 G16
+// R1, the split-K recipe's write-through form).
+__device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int n, float4 v) {
+  const int64_t e = ((int64_t)blockIdx.z * p.M + m) * p.ldp + n;
+  if (p.flags) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), partial_rsrc(p), (int)(e * 4), 0, 16);
+  } else {
+    *reinterpret_cast<float4*>(p.partial + e) = v;
+  }
+}
+
 // Output row offset (elements): plain row-major (out_rows_per_group == 0) or grouped rows.
 __device__ __forceinline__ int64_t out_off(const sp_conv_desc& d, int64_t m) {
   if (d.out_rows_per_group <= 0) return m * d.ldc;
@@ -168,7 +187,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
     if (m >= p.M || n >= p.d.Cout) continue;
     float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
     if (p.splits > 1) {
-      *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+      store_partial(p, m, n, v);
     } else {
       epilogue_store<BF>(p, m, n, v);
     }
@@ -231,7 +250,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         if (m >= p.M || n >= d.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
         if (p.splits > 1) {
-          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+          store_partial(p, m, n, v);
         } else if (fastv) {
           epilogue_vec<BF>(p, m, n, v, r1[u]);
         } else {
@@ -243,41 +262,45 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
 }
 
 // In-kernel split-K combine of output tile `tile` (BM × BN from m0, n0), called by every workgroup of a
-// split-K launch with p.flags set, after all of its threads stored their raw partial sums: the last of the
-// p.splits z slices to arrive (per-tile counter, agent-scope atomic: the slices may run on different XCDs,
-// whose L2s the release / acquire fences write back / invalidate) adds the partial slabs in fixed z order
-// 0, 1, ..., splits-1 — splitk_reduce_kernel's order, so the result is bit-identical to it and does not
-// depend on which slice came last — runs the fused epilogue and re-arms the counter for the next launch on
-// the stream. Replaces the reduce launch (one per split-K GEMM: 135 of a bs1 forward's ≈430 kernels).
-// lds_flag: one int of the kernel's own LDS, free by now.
+// split-K launch with p.flags set, after all of its threads stored their raw partial sums (store_partial,
+// write-through): the last of the p.splits z slices to arrive (per-tile ticket) adds the partial slabs in
+// fixed z order 0, 1, ..., splits-1 — splitk_reduce_kernel's order, so the result is bit-identical to it and
+// does not depend on which slice came last — runs the fused epilogue and re-arms the ticket for the next
+// launch on the stream. Replaces the reduce launch (one per split-K GEMM: 135 of a bs1 forward's ≈430).
+// Visibility across XCDs (their L2s are not coherent): every wave drains its sc1 slab stores, the workgroup
+// meets, ONE lane draws the ticket with a relaxed agent-scope add; the last arriver reads every slab with sc1
+// loads (cdna_hip_programming.md §6 G16, the split-K recipe's write-through form: no release / acquire
+// fence, which cost ≈2 µs per workgroup measured here). lds_flag: one int of the kernel's LDS array.
 template <int NT>
 __device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_t m0, int n0, int BM, int BN,
                                              int* lds_flag) {
-  __threadfence();  // release: this thread's partial stores
+  typedef __attribute__((address_space(1))) int gint;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  gint* ticket = (gint*)p.flags + tile;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through slab stores are done
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(p.flags + tile, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    *lds_flag = old == p.splits - 1;
-  }
+  if (threadIdx.x == 0)
+    *lds_flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
   __syncthreads();
   if (!*lds_flag) return;
-  __threadfence();  // acquire: every slice's partial stores
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below
+  const __amdgpu_buffer_rsrc_t rs = partial_rsrc(p);
   const int n4 = BN / 4;
-  const int64_t zs = p.M * p.ldp;
+  const int zs = (int)(p.M * p.ldp * 4);
   for (int idx = threadIdx.x; idx < BM * n4; idx += NT) {
     const int row = idx / n4;
     const int n = n0 + (idx - row * n4) * 4;
     const int64_t m = m0 + row;
     if (m >= p.M || n >= p.d.Cout) continue;
-    const float* src = p.partial + m * p.ldp + n;
-    float4 v = *reinterpret_cast<const float4*>(src);
+    const int off = (int)((m * p.ldp + n) * 4);
+    float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
     for (int z = 1; z < p.splits; ++z) {
-      const float4 u = *reinterpret_cast<const float4*>(src + z * zs);
+      const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + z * zs, 0, 16));
       v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
     }
     epilogue_store(p, m, n, v);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(p.flags + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Host side: keep the in-kernel combine only when every tile of the grid has its own counter.

@@ -3,7 +3,8 @@
 Implements the part of `RTDetrImageProcessorPil` that AmenitiesDetector uses
 (reference serve.py:67-68, 98, 103-109):
 
-* ``processor(images=PIL.Image, return_tensors="pt")`` → mapping with
+* ``processor(images=PIL.Image, return_tensors="pt")`` (or a GPU-decoded image from
+  ``spotter_amd.jpeg.open_image``, read in place) → mapping with
   ``pixel_values`` f32 ``[n, 3, 640, 640]`` (IPP:129-143 defaults: resize
   640×640 BILINEAR, rescale 1/255, no normalize, no pad), computed by the
   fused HIP kernel ``sp_preprocess_u8`` (bit-exact with Pillow).
@@ -42,6 +43,19 @@ class SpotterBatchFeature(dict):
             return self[k]
         except KeyError as e:
             raise AttributeError(k) from e
+
+
+def _device_rgb(img, dev):
+    """A uint8 [H, W, 3] device tensor already holding the image (a GPU-decoded DeviceRGBImage, or a CUDA
+    tensor given directly), else None."""
+    t = getattr(img, "spotter_device_rgb", None)
+    if t is None and torch.is_tensor(img) and img.is_cuda:
+        t = img
+    if t is None:
+        return None
+    if t.dtype != torch.uint8 or t.dim() != 3 or t.shape[2] != 3:
+        raise ValueError("device images must be uint8 [H, W, 3]")
+    return t.to(dev).contiguous()
 
 
 def _as_uint8_rgb(img) -> np.ndarray:
@@ -151,13 +165,16 @@ class SpotterImageProcessor:
             raise ValueError("images is required")
         if not isinstance(images, (list, tuple)):
             images = [images]
-        arrs = [_as_uint8_rgb(im) for im in images]
         dev = self._dev()
+        # GPU-decoded images (spotter_amd.jpeg.open_image) are read in place; the rest go up once, pinned
+        dimgs = [_device_rgb(im, dev) for im in images]
+        arrs = [_as_uint8_rgb(im) for im, d in zip(images, dimgs) if d is None]
         oh, ow = int(self.size["height"]), int(self.size["width"])
         with torch.cuda.device(dev):
-            ups = self._upload(arrs, dev)
-            out = torch.empty((len(arrs), 3, oh, ow), dtype=torch.float32, device=dev)
-            ops.preprocess_u8(ups, out, oh, ow)
+            ups = iter(self._upload(arrs, dev) if arrs else [])
+            srcs = [d if d is not None else next(ups) for d in dimgs]
+            out = torch.empty((len(srcs), 3, oh, ow), dtype=torch.float32, device=dev)
+            ops.preprocess_u8(srcs, out, oh, ow)
         if return_tensors not in ("pt", None):
             raise ValueError("only return_tensors='pt' is supported")
         return SpotterBatchFeature(pixel_values=out)

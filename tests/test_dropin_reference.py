@@ -145,6 +145,16 @@ def test_reference_process_single_image_flow_with_our_types(monkeypatch, tmp_pat
         assert images.mode == "RGB" and images.size == (1200, 717)
         return SpotterBatchFeature(pixel_values=torch.zeros(1, 3, 640, 640))
 
+    # no GPU here: the GPU JPEG decoder declines, so open_image takes the reference's own Image.open
+    from spotter_amd import jpeg
+
+    def no_gpu(device=None):
+        class _D:
+            def decode(self, data):
+                raise jpeg.UnsupportedJpeg("CPU test")
+        return _D()
+
+    monkeypatch.setattr(jpeg, "decoder", no_gpu)
     with patch.object(SpotterImageProcessor, "__call__", fake_proc), \
          patch.object(type(serve.model), "__call__", lambda self, **kw: SpotterDetectionOutput(logits, boxes)), \
          patch.object(SpotterImageProcessor, "post_process_object_detection", lambda self, *a, **k: fake_pp(*a, **k)):

@@ -1,0 +1,104 @@
+"""GPU: the JPEG decode step (sp_jpeg_to_rgb + the host entropy decoder) against Pillow's own decode, bit for
+bit, and the serve.py drop-in around it (spotter_amd.jpeg.open_image → SpotterImageProcessor)."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from PIL import Image, ImageDraw  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "test_pic.jpg")
+
+
+def _jpeg(img, mode="RGB", **kw):
+    b = io.BytesIO()
+    Image.fromarray(img).convert(mode).save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def _cases():
+    from spotter_amd.synthetic import synthetic_image
+
+    yield "test_pic", open(GOLDEN, "rb").read()
+    for (h, w) in [(1, 1), (2, 3), (17, 33), (233, 177), (480, 640), (720, 1280)]:
+        img = synthetic_image(h * 7 + w, h, w) if min(h, w) >= 2 else np.full((h, w, 3), 77, np.uint8)
+        for sub in (0, 1, 2):
+            for prog in (False, True):
+                yield f"{h}x{w} sub{sub} prog{int(prog)}", _jpeg(img, quality=90, subsampling=sub, progressive=prog)
+    yield "gray", _jpeg(synthetic_image(3, 45, 61), mode="L", quality=85)
+    yield "restart", _jpeg(synthetic_image(5, 123, 77), quality=80, restart_marker_rows=1, subsampling=2)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from spotter_amd._lib import lib
+
+    assert lib().sp_device_init(0) == 0, lib().sp_last_error()
+    return torch.device("cuda", 0)
+
+
+def test_gpu_decode_matches_pillow(dev):
+    from spotter_amd.jpeg import JpegDecoder
+
+    d = JpegDecoder(dev)
+    n = 0
+    for name, data in _cases():
+        got = d.decode(data).cpu().numpy()
+        ref = np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+        assert got.shape == ref.shape, name
+        bad = np.argwhere(got != ref)
+        assert bad.size == 0, f"{name}: {len(bad)} samples differ, first at {bad[:3].tolist()}"
+        n += 1
+    assert n > 30
+
+
+def test_open_image_is_a_lazy_pil_image(dev):
+    """open_image(bytes) → DeviceRGBImage: size / mode without a sync, convert("RGB") stays lazy, the host
+    pixels (np.asarray, ImageDraw, JPEG save — serve.py's draw / encode tail) equal Pillow's decode; PNG
+    bytes take the reference's Image.open."""
+    from spotter_amd.jpeg import DeviceRGBImage, open_image
+
+    data = open(GOLDEN, "rb").read()
+    ref = Image.open(io.BytesIO(data)).convert("RGB")
+    with open_image(data) as raw:
+        assert isinstance(raw, DeviceRGBImage)
+        im = raw.convert("RGB")
+        assert isinstance(im, DeviceRGBImage) and im.size == ref.size and im.mode == "RGB"
+        assert np.array_equal(np.asarray(im), np.asarray(ref))
+        d1, d2 = ImageDraw.Draw(im), ImageDraw.Draw(ref)
+        for d in (d1, d2):
+            d.rectangle([10, 10, 200, 100], outline="red", width=3)
+        assert np.array_equal(np.asarray(im), np.asarray(ref))
+        b = io.BytesIO()
+        im.save(b, format="JPEG")
+        assert b.getvalue()[:2] == b"\xff\xd8"
+    p = io.BytesIO()
+    ref.save(p, "PNG")
+    other = open_image(p.getvalue())
+    assert not isinstance(other, DeviceRGBImage) and other.convert("RGB").size == ref.size
+
+
+def test_processor_reads_the_device_image_in_place(dev):
+    """processor(images=open_image(bytes)) gives the same pixel_values as processor(images=Pillow's decode),
+    bit for bit, for the reference fixture and a 4:2:0 progressive JPEG, alone and batched with a PIL image."""
+    from spotter_amd import SpotterImageProcessor
+    from spotter_amd.jpeg import open_image
+    from spotter_amd.synthetic import synthetic_image
+
+    proc = SpotterImageProcessor()
+    datas = [open(GOLDEN, "rb").read(), _jpeg(synthetic_image(11, 480, 800), quality=88, subsampling=2,
+                                             progressive=True)]
+    for data in datas:
+        with open_image(data) as raw:
+            im = raw.convert("RGB")
+            a = proc(images=im)["pixel_values"]
+            assert getattr(im, "_im", None) is None  # the processor never pulled the host pixels
+        b = proc(images=Image.open(io.BytesIO(data)).convert("RGB"))["pixel_values"]
+        assert torch.equal(a, b)
+    mix = proc(images=[open_image(datas[0]).convert("RGB"), Image.open(io.BytesIO(datas[1])).convert("RGB")])
+    ref = proc(images=[Image.open(io.BytesIO(x)).convert("RGB") for x in datas])
+    assert torch.equal(mix["pixel_values"], ref["pixel_values"])

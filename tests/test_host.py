@@ -547,8 +547,9 @@ def test_dockerfile_copies_exist_in_their_contexts():
 
 
 def test_dropin_script_patches_serve_py(tmp_path):
-    """spotter_amd.dropin (run by the Dockerfile) on a copy of the reference serve.py: the two lines of
-    serve.py:203-204 are replaced, a second run is a no-op, and a serve.py whose lines moved is refused."""
+    """spotter_amd.dropin (run by the Dockerfile) on a copy of the reference serve.py: the lines of
+    serve.py:203-204 and the image open of serve.py:96 are replaced, a second run is a no-op, and a
+    serve.py whose lines moved is refused."""
     import sys
 
     from spotter_amd import dropin
@@ -556,8 +557,9 @@ def test_dropin_script_patches_serve_py(tmp_path):
     ref = "/root/reference/apps/spotter/src/spotter/serve.py"
     if os.path.exists(ref):
         src = open(ref).read()
-    else:  # the GPU box has no reference: the two lines as the reference writes them
-        src = f"import os\nmodel_name = os.environ.get('MODEL_NAME')\n{dropin.OLD_MODEL}\n{dropin.OLD_PROC}\n"
+    else:  # the GPU box has no reference: the three lines as the reference writes them
+        src = (f"import os\nmodel_name = os.environ.get('MODEL_NAME')\n            {dropin.OLD_OPEN}\n"
+               f"{dropin.OLD_MODEL}\n{dropin.OLD_PROC}\n")
     p = tmp_path / "serve.py"
     p.write_text(src)
     for _ in range(2):
@@ -567,7 +569,11 @@ def test_dropin_script_patches_serve_py(tmp_path):
     out = p.read_text()
     dropin.check(out)
     assert out.count("SpotterForObjectDetection.from_pretrained(model_name)") == 1
-    assert out.replace(dropin.NEW_MODEL, dropin.OLD_MODEL).replace(dropin.NEW_PROC, dropin.OLD_PROC) == src
+    assert out.count("with open_image(image_bytes) as img_raw:") == 1
+    back = out
+    for old, new in dropin.REPLACEMENTS:
+        back = back.replace(new, old)
+    assert back == src
     bad = tmp_path / "bad.py"
     bad.write_text(src.replace(dropin.OLD_PROC, "processor = AutoImageProcessor.from_pretrained(other)"))
     r = subprocess.run([sys.executable, "-m", "spotter_amd.dropin", str(bad)], cwd=ROOT, capture_output=True,

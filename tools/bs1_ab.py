@@ -64,6 +64,11 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1))
             res[key]["ms"].append(round(float(np.median(ts)), 4))
+    for key, r in runners.items():  # after hundreds of replays: still the same outputs
+        lg, bx = r(x)
+        torch.cuda.synchronize()
+        res[key]["bit_identical_after_replays"] = bool(np.array_equal(lg.cpu().numpy(), ref[0])
+                                                       and np.array_equal(bx.cpu().numpy(), ref[1]))
     for key, v in res.items():
         v["median_ms"] = round(float(np.median(v["ms"])), 4)
         print(json.dumps({"variant": key, **v}), flush=True)
