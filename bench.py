@@ -603,8 +603,11 @@ def main():
             from tools.latency import measure
 
             lat_model = SpotterForObjectDetection(PRESETS[args.preset], use_graphs=True)
-            lat = measure(args.preset, args.latency_iters, graphs=True, model=lat_model)
+            lat = measure(args.preset, args.latency_iters, graphs=True, model=lat_model)  # GPU JPEG decode
             lat["full_request"] = detect_path.measure(args.preset, args.latency_iters, model=lat_model)
+            # the same core with the reference's host decode (Pillow), for the decode stage's comparison
+            h = measure(args.preset, max(20, args.latency_iters // 2), graphs=True, model=lat_model, decode="host")
+            lat["host_decode"] = {k: h[k] for k in ("p50_ms", "p95_ms", "stages_p50_ms")}
         except Exception as e:
             lat = {"error": f"{type(e).__name__}: {e}"}
 

@@ -161,8 +161,10 @@ int sp_conv2d(const sp_conv_desc* d, void* stream);
  * the CALLING THREAD (-1, the default, = chosen by shape). Nothing on the product path calls it, and
  * no environment variable is read: the production tile choice cannot be changed from outside. */
 int sp_set_conv_config(int cfg);
-/* The same override for split-K launches only (ABI v11; -1 = the library's choice): bs1 tile tuning. */
-int sp_set_splitk_config(int cfg);
+/* The same override for split-K launches only (ABI v11; cfg -1 = the library's choice), a cap on the split-K
+ * factor of this thread's later launches (max_splits < 1 = the default, 16) and the fewest 32-deep k-tiles a
+ * launch needs to split at all (min_ktiles < 1 = the default, 8): bs1 tuning hooks. */
+int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles);
 
 /* 3x3 stride-1 pad-1 convolution by Winograd F(2x2, 3x3) (ABI v9): the same result contract as
  * sp_conv2d on the same descriptor (KH = KW = 3, stride 1, pad 1; act, scale / shift, res1 / res2 as

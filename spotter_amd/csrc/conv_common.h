@@ -271,11 +271,9 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
 // meets, ONE lane draws the ticket with a relaxed agent-scope add; the last arriver reads every slab with sc1
 // loads (cdna_hip_programming.md §6 G16, the split-K recipe's write-through form: no release / acquire
 // fence, which cost ≈2 µs per workgroup measured here). lds_flag: one int of the kernel's LDS array.
-template <int NT>
-__device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_t m0, int n0, int BM, int BN,
-                                             int* lds_flag) {
+template <int NT, int BM, int BN>
+__device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_t m0, int n0, int* lds_flag) {
   typedef __attribute__((address_space(1))) int gint;
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   gint* ticket = (gint*)p.flags + tile;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through slab stores are done
   __syncthreads();
@@ -285,20 +283,48 @@ __device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_
   if (!*lds_flag) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below
   const __amdgpu_buffer_rsrc_t rs = partial_rsrc(p);
-  const int n4 = BN / 4;
   const int zs = (int)(p.M * p.ldp * 4);
-  for (int idx = threadIdx.x; idx < BM * n4; idx += NT) {
-    const int row = idx / n4;
-    const int n = n0 + (idx - row * n4) * 4;
-    const int64_t m = m0 + row;
-    if (m >= p.M || n >= p.d.Cout) continue;
-    const int off = (int)((m * p.ldp + n) * 4);
-    float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-    for (int z = 1; z < p.splits; ++z) {
-      const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off + z * zs, 0, 16));
-      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  constexpr int N4 = BN / 4, TOT = BM * N4;
+  constexpr int P = 4, ZC = 4;  // float4 positions per thread and slabs per round: 16 loads in flight
+  for (int base = threadIdx.x; base < TOT; base += NT * P) {
+    int off[P];
+    bool ok[P];
+    int64_t mm[P];
+    int nn[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const int idx = base + q * NT;
+      const int row = idx / N4;
+      nn[q] = n0 + (idx - row * N4) * 4;
+      mm[q] = m0 + row;
+      ok[q] = idx < TOT && mm[q] < p.M && nn[q] < p.d.Cout;
+      off[q] = ok[q] ? (int)((mm[q] * p.ldp + nn[q]) * 4) : 0;
     }
-    epilogue_store(p, m, n, v);
+    float4 acc[P];
+    for (int z0 = 0; z0 < p.splits; z0 += ZC) {
+      float4 u[ZC][P];
+#pragma unroll
+      for (int zz = 0; zz < ZC; ++zz) {  // every load issued before any is used (no per-slab wait chain)
+        const int z = z0 + zz < p.splits ? z0 + zz : p.splits - 1;
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+          u[zz][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[q] + z * zs, 0, 16));
+      }
+#pragma unroll
+      for (int zz = 0; zz < ZC; ++zz)
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          const float4 v = u[zz][q];
+          if (z0 + zz == 0) {
+            acc[q] = v;
+          } else if (z0 + zz < p.splits) {  // fixed z order: the splitk_reduce_kernel sums, bit for bit
+            acc[q].x += v.x; acc[q].y += v.y; acc[q].z += v.z; acc[q].w += v.w;
+          }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+      if (ok[q]) epilogue_store(p, mm[q], nn[q], acc[q]);
   }
   if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

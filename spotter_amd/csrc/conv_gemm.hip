@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
                       n0 + wn * TN * 32, lane);
   if (p.splits > 1 && p.flags) {
     __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<256>(p, blockIdx.y * gridDim.x + blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+    splitk_fixup<256, BM, BN>(p, blockIdx.y * gridDim.x + blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -278,6 +278,8 @@ int launch(const ConvArgs& a, hipStream_t s) {
 thread_local int g_forced_cfg = -1;
 // The same override for the split-K launches only (sp_set_splitk_config; bs1 tuning, tools/tune_bs1.py).
 thread_local int g_forced_splitk_cfg = -1;
+thread_local int g_splitk_max = 16;  // split-K factor cap (tuning: sp_set_splitk_config's second argument)
+thread_local int g_splitk_min_nk = 8;  // fewest k-tiles a launch must have to split (third argument)
 
 // Tile of a split-K launch on the bf16 / split MFMA kernels (the bs1 path): the test / tuning override, else
 // the 64×64 register-staged tile.
@@ -305,8 +307,10 @@ extern "C" int sp_set_conv_config(int cfg) {
   return 0;
 }
 
-extern "C" int sp_set_splitk_config(int cfg) {
+extern "C" int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles) {
   sp::g_forced_splitk_cfg = cfg < 0 ? -1 : cfg;
+  sp::g_splitk_max = max_splits < 1 ? 16 : (max_splits > 16 ? 16 : max_splits);
+  sp::g_splitk_min_nk = min_ktiles < 1 ? 8 : min_ktiles;
   return 0;
 }
 
@@ -385,12 +389,13 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     // ≥ 8 k-tiles each; tiny-M linears (< 64 tiles) split even at K = 256; grids of up to
     // SP_SPLITK_BLOCKS tiles split only when each workgroup would walk ≥ 64 k-tiles.
     int sp = 1;
-    if (blocks64 < 64 && nk >= 8 && nk < 16) sp = nk / 4;
+    if (nk < g_splitk_min_nk) sp = 1;
+    else if (blocks64 < 64 && nk >= 8 && nk < 16) sp = nk / 4;
     else if (blocks64 < 256 && nk >= 16) sp = (int)((512 + blocks64 - 1) / blocks64), sp = sp < nk / 8 ? sp : nk / 8;
     else if (blocks64 < SP_SPLITK_BLOCKS && nk >= 64) sp = (int)((SP_SPLITK_BLOCKS + blocks64 - 1) / blocks64);
     // split-K runs on the register-staged tiles (fp32 A) and reduces through the fp32-row epilogue
     if (d->workspace && sp > 1 && !d->A_bf16 && !d->C_bf16 && !d->res1_bf16 && !d->res2_bf16) {
-      if (sp > 16) sp = 16;
+      if (sp > g_splitk_max) sp = g_splitk_max;
       while (sp > 1 && (int64_t)sp * a.M * a.ldp > d->workspace_elems) --sp;
       if (sp > 1) a.splits = sp;
     }

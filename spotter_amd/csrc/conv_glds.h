@@ -560,8 +560,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
     __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
     const int tilesN = (p.d.Cout + C::BN - 1) / C::BN;
     const int mt = wg / tilesN;
-    splitk_fixup<C::NT>(p, blockIdx.x, (int64_t)mt * C::BM, (wg - mt * tilesN) * C::BN, C::BM, C::BN,
-                        reinterpret_cast<int*>(smem));
+    splitk_fixup<C::NT, C::BM, C::BN>(p, blockIdx.x, (int64_t)mt * C::BM, (wg - mt * tilesN) * C::BN,
+                                       reinterpret_cast<int*>(smem));
   }
 #if SP_GLDS_STAMP
   __syncthreads();

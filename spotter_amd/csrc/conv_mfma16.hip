@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
                             lane);
   if (p.splits > 1 && p.flags) {
     __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
                             lane);
   if (p.splits > 1 && p.flags) {
     __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -518,21 +518,23 @@ int launch_pipe(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
+  ConvArgs b = a;
+  splitk_flags_fit(b, tiles);
   // NS stages of the fp32 A tile + PL bf16 B planes must fit the 160 KiB LDS
   constexpr bool fits3 = NS * (BM * 8 + 3 * BN * 4) * 16 <= 163840;
   if (planes == 3) {
     if constexpr (fits3) {
-      hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+      hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, b);
     } else {
       set_error("sp_conv2d: pipe tile %dx%d with %d stages does not fit LDS in f32x3 mode", BM, BN, NS);
       return -1;
     }
   } else {
-    hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, b);
   }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 pipe)" : "sp_conv2d(bf16 pipe)");
-  if (rc || a.splits == 1) return rc;
-  return launch_splitk_reduce(a, s);
+  if (rc || b.splits == 1 || b.flags) return rc;
+  return launch_splitk_reduce(b, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -736,7 +738,7 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
                             lane);
   if (p.splits > 1 && p.flags) {
     __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT>(p, blockIdx.x, m0, n0, BM, BN, reinterpret_cast<int*>(smem));
+    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -749,13 +751,15 @@ int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
+  ConvArgs b = a;
+  splitk_flags_fit(b, tiles);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 3>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 3>), grid, dim3(512), 0, s, b);
   else
-    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 1>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 1>), grid, dim3(512), 0, s, b);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 ping-pong)" : "sp_conv2d(bf16 ping-pong)");
-  if (rc || a.splits == 1) return rc;
-  return launch_splitk_reduce(a, s);
+  if (rc || b.splits == 1 || b.flags) return rc;
+  return launch_splitk_reduce(b, s);
 }
 
 

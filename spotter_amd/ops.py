@@ -305,12 +305,13 @@ def force_conv_config(cfg=None):
     lib().sp_set_conv_config(-1 if cfg in (None, "", "-") else int(cfg))
 
 
-def force_splitk_config(cfg=None):
-    """Tuning tools: pin the tile configuration of this thread's later split-K launches only
-    (sp_set_splitk_config); None restores the library's choice."""
+def force_splitk_config(cfg=None, max_splits=None, min_ktiles=None):
+    """Tuning tools: pin the tile configuration of this thread's later split-K launches only, cap their
+    split-K factor and set the fewest k-tiles that split (sp_set_splitk_config); None restores the default."""
     from ._lib import lib
 
-    lib().sp_set_splitk_config(-1 if cfg in (None, "", "-") else int(cfg))
+    lib().sp_set_splitk_config(-1 if cfg in (None, "", "-") else int(cfg), 0 if max_splits is None else int(max_splits),
+                               0 if min_ktiles is None else int(min_ktiles))
 
 
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):

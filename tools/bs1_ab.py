@@ -26,7 +26,8 @@ def main():
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="reduce:4,inkernel:4,inkernel:14,inkernel:66,inkernel:67,inkernel:68")
+    ap.add_argument("--variants", default="reduce:4:16,inkernel:4:16,reduce:66:16,reduce:67:16,reduce:67:4,"
+                                          "reduce:67:2,reduce:4:1")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = PRESETS[a.preset]
@@ -34,12 +35,14 @@ def main():
     eng = Engine(cfg, generate(cfg, seed=0), dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
-    variants = [v.split(":") for v in a.variants.split(",")]
+    dflt = ["reduce", "-1", "16", "8"]  # combine : split-K tile : max splits : min k-tiles to split
+    variants = [(lambda q: q + dflt[len(q):])(v.split(":")) for v in a.variants.split(",")]
     runners, ref = {}, None
     res = {}
-    for mode, c in variants:
-        eng.splitk_inkernel = mode == "inkernel"
-        ops.force_splitk_config(c)
+    for mode, c, ms, mk in variants:
+        eng.splitk_inkernel = mode.startswith("inkernel")
+        eng.fuse_ln = mode.endswith("ln")  # "reduce_ln" / "inkernel_ln": post-LNs fused into the GEMM epilogue
+        ops.force_splitk_config(c, int(ms), int(mk))
         try:
             r = GraphRunner(eng, 1, cfg.image_size, cfg.image_size)
         finally:
@@ -49,7 +52,7 @@ def main():
         out = (lg.cpu().numpy().copy(), bx.cpu().numpy().copy())
         if ref is None:
             ref = out
-        key = f"{mode}:{c}"
+        key = f"{mode}:{c}:{ms}:{mk}"
         runners[key] = r
         res[key] = {"max_dlogit": float(np.abs(out[0] - ref[0]).max()), "max_dbox": float(np.abs(out[1] - ref[1]).max()),
                     "bit_identical": bool(np.array_equal(out[0], ref[0]) and np.array_equal(out[1], ref[1])), "ms": []}

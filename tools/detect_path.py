@@ -1,6 +1,7 @@
 """p50 / p95 of the WHOLE /detect request on one replica, end to end:
 
-    request JSON → URL validation → HTTP fetch (local server) → JPEG decode → processor → model
+    request JSON → URL validation → HTTP fetch (local server) → JPEG decode (GPU, the drop-in's open_image;
+    --decode host: Pillow as the reference) → processor → model
     → post_process → id2label + amenity filter → draw boxes/labels → JPEG re-encode → base64
     → response JSON
 
@@ -64,16 +65,29 @@ def serve_bytes(payload: bytes):
     return srv, f"http://127.0.0.1:{srv.server_address[1]}/test_pic.jpg"
 
 
-async def process_image(client, url, proc, model, stamps):
+def opener(decode: str):
+    """serve.py:96's image open: the drop-in's open_image (GPU JPEG decode) or, with
+    decode="host", the reference's own Image.open."""
+    if decode == "gpu":
+        from spotter_amd.jpeg import open_image
+
+        return open_image
+    from PIL import Image
+
+    return lambda data: Image.open(io.BytesIO(data))
+
+
+async def process_image(client, url, proc, model, stamps, open_fn=None):
     """One image of a /detect request (serve.py:79-148 order), with per-stage time stamps."""
     import torch
-    from PIL import Image, ImageDraw
+    from PIL import ImageDraw
 
+    open_fn = open_fn or opener("gpu")
     t0 = time.perf_counter()
     r = await client.get(url)
     r.raise_for_status()
     t1 = time.perf_counter()
-    with Image.open(io.BytesIO(r.content)) as raw:
+    with open_fn(r.content) as raw:
         image = raw.convert("RGB")
         t2 = time.perf_counter()
         inputs = proc(images=image, return_tensors="pt").to("cpu")
@@ -102,7 +116,7 @@ async def process_image(client, url, proc, model, stamps):
     return {"url": url, "detections": found, "labeled_image_base64": b64}
 
 
-async def handle(body: bytes, client, proc, model, stamps):
+async def handle(body: bytes, client, proc, model, stamps, open_fn=None):
     """serve.py:179-196: parse the request, process its images, build the response JSON."""
     from pydantic import BaseModel, HttpUrl
 
@@ -110,13 +124,14 @@ async def handle(body: bytes, client, proc, model, stamps):
         image_urls: list[HttpUrl]
 
     req = DetectionRequest.model_validate(json.loads(body))
-    results = await asyncio.gather(*[process_image(client, str(u), proc, model, stamps) for u in req.image_urls])
+    results = await asyncio.gather(*[process_image(client, str(u), proc, model, stamps, open_fn)
+                                     for u in req.image_urls])
     found = sorted({d["label"] for r in results for d in r["detections"]})
     desc = f"The property contains: {', '.join(found)}." if found else "No relevant amenities detected."
     return json.dumps({"amenities_description": desc, "images": results})
 
 
-def measure(preset="r101vd", iters=200, model=None):
+def measure(preset="r101vd", iters=200, model=None, decode="gpu"):
     import httpx
     import numpy as np
     import torch
@@ -130,13 +145,14 @@ def measure(preset="r101vd", iters=200, model=None):
     model = model or SpotterForObjectDetection(PRESETS[preset], use_graphs=True)
     proc = SpotterImageProcessor()
     body = json.dumps({"image_urls": [url]}).encode()
+    open_fn = opener(decode)
 
     async def run():
         stamps, total = {}, []
         async with httpx.AsyncClient() as client:
             for i in range(iters + 5):
                 t0 = time.perf_counter()
-                await handle(body, client, proc, model, stamps if i >= 5 else {})
+                await handle(body, client, proc, model, stamps if i >= 5 else {}, open_fn)
                 if i >= 5:
                     total.append((time.perf_counter() - t0) * 1e3)
         return stamps, total
@@ -151,7 +167,7 @@ def measure(preset="r101vd", iters=200, model=None):
                       "preprocess, forward, post-process, labels, draw, JPEG re-encode, base64, response JSON), "
                       "bs1, 1200x717 JPEG",
             "p50_ms": round(float(np.percentile(total, 50)), 3), "p95_ms": round(float(np.percentile(total, 95)), 3),
-            "iters": iters, "preset": preset,
+            "iters": iters, "preset": preset, "decode": decode,
             "stages_p50_ms": {k: round(float(np.percentile(v, 50)), 3) for k, v in stamps.items()}}
 
 
@@ -159,8 +175,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--preset", default="r101vd")
+    ap.add_argument("--decode", default="gpu", choices=["gpu", "host"])
     a = ap.parse_args()
-    print(json.dumps(measure(a.preset, a.iters)))
+    print(json.dumps(measure(a.preset, a.iters, decode=a.decode)))
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 """p50/p95 latency of the /detect core at batch 1 (serve.py:96-117 minus HTTP/draw/JPEG):
-JPEG decode → processor → model → post_process → labels/boxes on the host.
+JPEG decode (GPU by default, as the drop-in's open_image; --decode host: Pillow) → processor → model →
+post_process → labels/boxes on the host.
 
     python tools/latency.py [--iters 200] [--no-graph]
 """
@@ -19,8 +20,18 @@ from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
 from spotter_amd.config import PRESETS
 
 
-def measure(preset="r101vd", iters=200, graphs=True, model=None):
-    """p50/p95 of the bs1 /detect core on the test fixture JPEG, plus the GPU-only forward p50."""
+def measure(preset="r101vd", iters=200, graphs=True, model=None, decode="gpu"):
+    """p50/p95 of the bs1 /detect core on the test fixture JPEG, plus the GPU-only forward p50. decode: "gpu"
+    opens the image with the drop-in's open_image (serve.py:96 as INTEGRATION.md §2 changes it: JPEG decoded
+    on the GPU, host pixels fetched lazily), "host" with the reference's Image.open (Pillow on the CPU)."""
+    if decode == "gpu":
+        from spotter_amd.jpeg import open_image
+
+        def open_fn(b):
+            return open_image(b)
+    else:
+        def open_fn(b):
+            return Image.open(io.BytesIO(b))
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     with open(os.path.join(root, "tests", "golden", "test_pic.jpg"), "rb") as f:
         jpeg = f.read()
@@ -28,7 +39,7 @@ def measure(preset="r101vd", iters=200, graphs=True, model=None):
     proc = SpotterImageProcessor()
 
     def detect():
-        with Image.open(io.BytesIO(jpeg)) as raw:
+        with open_fn(jpeg) as raw:
             image = raw.convert("RGB")
             inputs = proc(images=image, return_tensors="pt").to("cpu")
             with torch.no_grad():
@@ -47,7 +58,7 @@ def measure(preset="r101vd", iters=200, graphs=True, model=None):
         t0 = time.perf_counter()
         detect()
         ts.append(time.perf_counter() - t0)
-    with Image.open(io.BytesIO(jpeg)) as raw:
+    with open_fn(jpeg) as raw:
         x = proc(images=raw.convert("RGB"))["pixel_values"]
     fw = []
     for _ in range(50):
@@ -60,7 +71,7 @@ def measure(preset="r101vd", iters=200, graphs=True, model=None):
     stages = {"decode": [], "processor": [], "model": [], "post_process": []}
     for _ in range(min(iters, 50)):
         t0 = time.perf_counter()
-        with Image.open(io.BytesIO(jpeg)) as raw:
+        with open_fn(jpeg) as raw:
             image = raw.convert("RGB")
         t1 = time.perf_counter()
         inputs = proc(images=image, return_tensors="pt").to("cpu")
@@ -79,7 +90,7 @@ def measure(preset="r101vd", iters=200, graphs=True, model=None):
     ts, fw = np.array(ts) * 1e3, np.array(fw) * 1e3
     return {"metric": "p50 /detect core latency (bs1, 1200x717 JPEG: decode, preprocess, forward, "
                       "post_process, labels/boxes to host)", "graphs": graphs,
-            "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
+            "decode": decode, "p50_ms": round(float(np.percentile(ts, 50)), 3), "p95_ms": round(float(np.percentile(ts, 95)), 3),
             "forward_p50_ms": round(float(np.percentile(fw, 50)), 3), "iters": iters, "preset": preset,
             "stages_p50_ms": {k: round(float(np.percentile(v, 50)), 3) for k, v in stages.items()}}
 
@@ -89,8 +100,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--decode", default="gpu", choices=["gpu", "host"])
     a = ap.parse_args()
-    print(json.dumps(measure(a.preset, a.iters, not a.no_graph)))
+    print(json.dumps(measure(a.preset, a.iters, not a.no_graph, decode=a.decode)))
 
 
 if __name__ == "__main__":
