@@ -113,13 +113,6 @@ typedef struct {
   uint16_t* C_bf16;
   const uint16_t* res1_bf16;
   const uint16_t* res2_bf16;
-  /* ABI v11: in-kernel split-K combine. With a workspace and split-K, splitk_flags (non-NULL) is an array of
-   * splitk_flags_len int32 arrival counters that must be ZERO before the call and are zero again when the
-   * launch completes (the same array can serve every sp_conv2d call of one stream): the last workgroup of
-   * each output tile to finish adds the partial sums in fixed z order (bit-identical to the separate reduce
-   * launch used when splitk_flags is NULL or shorter than the tile grid) and applies the epilogue. */
-  int32_t* splitk_flags;
-  int64_t splitk_flags_len;
 } sp_conv_desc;
 
 /*

@@ -44,7 +44,6 @@ class SpConvDesc(C.Structure):
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
         ("C_bf16", vp), ("res1_bf16", vp), ("res2_bf16", vp),
-        ("splitk_flags", vp), ("splitk_flags_len", i64),
     ]
 
 

@@ -36,31 +36,7 @@ struct ConvArgs {
   // producer instead of split per fragment in the GEMM (lda and bs_a count bf16 elements then).
   const uint16_t* A16 = nullptr;
   int64_t a_plane_stride = 0;
-  // In-kernel split-K combine (ABI v11, sp_conv_desc.splitk_flags): one zeroed arrival counter per
-  // output tile (indexed by the tile's x / y grid position, shared by its z slices); null = the
-  // separate splitk_reduce launch. Launchers clear it when the grid has more tiles than counters.
-  int32_t* flags = nullptr;
-  int64_t flags_len = 0;
 };
-
-// Buffer resource over the split-K partial slabs (wave-uniform: built from kernel arguments only).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t partial_rsrc(const ConvArgs& p) {
-  return __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, (int)(p.splits * p.M * p.ldp * 4), 0x00020000);
-}
-
-// Raw partial sums of row m, channels n..n+3 of z slice blockIdx.z. With the in-kernel combine (p.flags) the
-// slab is stored write-through (sc1: the line leaves this XCD's L2 at once), so the last-arriving slice on
-// any XCD reads it with sc1 loads and neither side needs a cache-wide fence (cdna_hip_programming.md §6 G16
-// R1, the split-K recipe's write-through form).
-__device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int n, float4 v) {
-  const int64_t e = ((int64_t)blockIdx.z * p.M + m) * p.ldp + n;
-  if (p.flags) {
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), partial_rsrc(p), (int)(e * 4), 0, 16);
-  } else {
-    *reinterpret_cast<float4*>(p.partial + e) = v;
-  }
-}
 
 // Output row offset (elements): plain row-major (out_rows_per_group == 0) or grouped rows.
 __device__ __forceinline__ int64_t out_off(const sp_conv_desc& d, int64_t m) {
@@ -187,7 +163,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
     if (m >= p.M || n >= p.d.Cout) continue;
     float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
     if (p.splits > 1) {
-      store_partial(p, m, n, v);
+      *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
     } else {
       epilogue_store<BF>(p, m, n, v);
     }
@@ -250,7 +226,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         if (m >= p.M || n >= d.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
         if (p.splits > 1) {
-          store_partial(p, m, n, v);
+          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
         } else if (fastv) {
           epilogue_vec<BF>(p, m, n, v, r1[u]);
         } else {
@@ -259,79 +235,6 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
       }
     }
   }
-}
-
-// In-kernel split-K combine of output tile `tile` (BM × BN from m0, n0), called by every workgroup of a
-// split-K launch with p.flags set, after all of its threads stored their raw partial sums (store_partial,
-// write-through): the last of the p.splits z slices to arrive (per-tile ticket) adds the partial slabs in
-// fixed z order 0, 1, ..., splits-1 — splitk_reduce_kernel's order, so the result is bit-identical to it and
-// does not depend on which slice came last — runs the fused epilogue and re-arms the ticket for the next
-// launch on the stream. Replaces the reduce launch (one per split-K GEMM: 135 of a bs1 forward's ≈430).
-// Visibility across XCDs (their L2s are not coherent): every wave drains its sc1 slab stores, the workgroup
-// meets, ONE lane draws the ticket with a relaxed agent-scope add; the last arriver reads every slab with sc1
-// loads (cdna_hip_programming.md §6 G16, the split-K recipe's write-through form: no release / acquire
-// fence, which cost ≈2 µs per workgroup measured here). lds_flag: one int of the kernel's LDS array.
-template <int NT, int BM, int BN>
-__device__ __forceinline__ void splitk_fixup(const ConvArgs& p, int tile, int64_t m0, int n0, int* lds_flag) {
-  typedef __attribute__((address_space(1))) int gint;
-  gint* ticket = (gint*)p.flags + tile;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through slab stores are done
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *lds_flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.splits - 1;
-  __syncthreads();
-  if (!*lds_flag) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below
-  const __amdgpu_buffer_rsrc_t rs = partial_rsrc(p);
-  const int zs = (int)(p.M * p.ldp * 4);
-  constexpr int N4 = BN / 4, TOT = BM * N4;
-  constexpr int P = 4, ZC = 4;  // float4 positions per thread and slabs per round: 16 loads in flight
-  for (int base = threadIdx.x; base < TOT; base += NT * P) {
-    int off[P];
-    bool ok[P];
-    int64_t mm[P];
-    int nn[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const int idx = base + q * NT;
-      const int row = idx / N4;
-      nn[q] = n0 + (idx - row * N4) * 4;
-      mm[q] = m0 + row;
-      ok[q] = idx < TOT && mm[q] < p.M && nn[q] < p.d.Cout;
-      off[q] = ok[q] ? (int)((mm[q] * p.ldp + nn[q]) * 4) : 0;
-    }
-    float4 acc[P];
-    for (int z0 = 0; z0 < p.splits; z0 += ZC) {
-      float4 u[ZC][P];
-#pragma unroll
-      for (int zz = 0; zz < ZC; ++zz) {  // every load issued before any is used (no per-slab wait chain)
-        const int z = z0 + zz < p.splits ? z0 + zz : p.splits - 1;
-#pragma unroll
-        for (int q = 0; q < P; ++q)
-          u[zz][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[q] + z * zs, 0, 16));
-      }
-#pragma unroll
-      for (int zz = 0; zz < ZC; ++zz)
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-          const float4 v = u[zz][q];
-          if (z0 + zz == 0) {
-            acc[q] = v;
-          } else if (z0 + zz < p.splits) {  // fixed z order: the splitk_reduce_kernel sums, bit for bit
-            acc[q].x += v.x; acc[q].y += v.y; acc[q].z += v.z; acc[q].w += v.w;
-          }
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < P; ++q)
-      if (ok[q]) epilogue_store(p, mm[q], nn[q], acc[q]);
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Host side: keep the in-kernel combine only when every tile of the grid has its own counter.
-inline void splitk_flags_fit(ConvArgs& a, int64_t tiles) {
-  if (a.splits <= 1 || tiles > a.flags_len) a.flags = nullptr;
 }
 
 // Row-LayerNorm epilogue (sp_conv_desc.ln_gamma): the workgroup holds whole output rows — BM = 32 rows

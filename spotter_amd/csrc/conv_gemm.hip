@@ -238,10 +238,6 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   for (int i = 0; i < TM; ++i)
     epilogue_band<TN>(p, smem + wave * (32 * TN * 32), acc[i], m0 + wm * TM * 32 + i * 32,
                       n0 + wn * TN * 32, lane);
-  if (p.splits > 1 && p.flags) {
-    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<256, BM, BN>(p, blockIdx.y * gridDim.x + blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
-  }
 }
 
 // Split-K combine: out = epilogue(Σ_z partial[z]) in fixed z order (deterministic).
@@ -264,29 +260,21 @@ template <int TM, int TN, int DB, int WM = 2, bool LN = false>
 int launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * (4 / WM) * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM), a.splits);
-  ConvArgs b = a;
-  splitk_flags_fit(b, (int64_t)grid.x * grid.y);
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, b);
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, a);
   int rc = check_launch("sp_conv2d");
-  if (rc || b.splits == 1 || b.flags) return rc;
-  return launch_splitk_reduce(b, s);
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
 }
 
 // Tile override for tests and tuning tools, set explicitly per thread by sp_set_conv_config (never
 // from the environment): "<TM><TN><DB>" for the fp32 kernel (e.g. 221) or the conv_mfma16 config
 // number (bf16 / split kernels); -1 = by shape (the production choice).
 thread_local int g_forced_cfg = -1;
-// The same override for the split-K launches only (sp_set_splitk_config; bs1 tuning, tools/tune_bs1.py).
+// bs1 tuning hooks (sp_set_splitk_config): the tile of split-K launches, the split-factor cap and the fewest
+// k-tiles that split
 thread_local int g_forced_splitk_cfg = -1;
-thread_local int g_splitk_max = 16;  // split-K factor cap (tuning: sp_set_splitk_config's second argument)
-thread_local int g_splitk_min_nk = 8;  // fewest k-tiles a launch must have to split (third argument)
-
-// Tile of a split-K launch on the bf16 / split MFMA kernels (the bs1 path): the test / tuning override, else
-// the 64×64 register-staged tile.
-int splitk_cfg() {
-  if (g_forced_splitk_cfg >= 0) return g_forced_splitk_cfg;
-  return 4;
-}
+thread_local int g_splitk_max = 16;
+thread_local int g_splitk_min_nk = 8;
 
 }  // namespace
 
@@ -380,8 +368,6 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   a.splits = 1;
   a.ldp = (d->Cout + 3) & ~3;
   a.partial = d->workspace;
-  a.flags = d->splitk_flags;
-  a.flags_len = d->splitk_flags ? d->splitk_flags_len : 0;
   {
     const int64_t blocks64 = ((a.M + 63) / 64) * ((d->Cout + 63) / 64);
     const int nk = (a.K + BK - 1) / BK;
@@ -419,7 +405,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   int cfg = forced_cfg();
   if (cfg < 0 && a.splits == 1)
     cfg = tile_table_lookup(a.M, d->Cout, a.K, d->KH, d->stride, planes);
-  if (cfg < 0 && a.splits > 1 && planes) cfg = splitk_cfg();
+  if (cfg < 0 && a.splits > 1 && planes && g_forced_splitk_cfg >= 0) cfg = g_forced_splitk_cfg;
   if (planes) return launch_mfma16(a, planes, cfg, s);
   if (a.splits > 1) return launch<1, 1, 0>(a, s);
   switch (cfg) {

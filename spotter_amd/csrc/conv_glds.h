@@ -556,13 +556,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
   ConvArgs q = p;
   q.d.C += (int64_t)bi * p.bs_c;
   glds_epilogue<WM, WN, TM, TN, PL, NS, BK, M16, APL, EPV>(q, smem, wg, acc, acc4);
-  if (p.splits > 1 && p.flags) {  // split-K never runs batched (launch_glds refuses it)
-    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    const int tilesN = (p.d.Cout + C::BN - 1) / C::BN;
-    const int mt = wg / tilesN;
-    splitk_fixup<C::NT, C::BM, C::BN>(p, blockIdx.x, (int64_t)mt * C::BM, (wg - mt * tilesN) * C::BN,
-                                       reinterpret_cast<int*>(smem));
-  }
 #if SP_GLDS_STAMP
   __syncthreads();
   GLDS_STAMP(3);
@@ -614,7 +607,6 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   }
   ConvArgs ab = a;
   ab.tiles_per_batch = (int32_t)per;
-  splitk_flags_fit(ab, tiles);
   dim3 grid((unsigned)tiles, 1, a.splits);
   // the 1×1 fast path where it applies, else the general implicit GEMM
   const bool t1 = t1_ok(a);
@@ -660,8 +652,8 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1, 1, 1>), grid, blk, 0, s, ab);
   }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 glds)" : "sp_conv2d(bf16 glds)");
-  if (rc || ab.splits == 1 || ab.flags) return rc;
-  return launch_splitk_reduce(ab, s);
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
 }
 
 
@@ -699,10 +691,7 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(62, 4, 1, 1, 8, 2, 32, false, 1, false)    /* 128×256, 4 waves of 32×256 */ \
   X(63, 8, 1, 1, 4, 2, 32, false, 1, true)    /* 256×128, 8 waves of 32×128 */ \
   X(64, 4, 1, 1, 4, 3, 32, false, 1, true)    /* 128×128, 4 waves of 32×128, 3 stages */ \
-  X(65, 8, 1, 1, 4, 2, 32, true, 1, false)     /* cfg 63 on 16x16x32 MFMAs */ \
-  X(66, 2, 2, 1, 1, 4, 32, false, 1, false)    /* 64×64, 4 stages (split-K at bs1: 3 k-tiles in flight) */ \
-  X(67, 2, 2, 1, 1, 6, 32, false, 1, false)    /* 64×64, 6 stages */ \
-  X(68, 2, 2, 1, 2, 4, 32, false, 1, false)    /* 64×128, 4 stages */
+  X(65, 8, 1, 1, 4, 2, 32, true, 1, false)     /* cfg 63 on 16x16x32 MFMAs */
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path

@@ -283,10 +283,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
-  if (p.splits > 1 && p.flags) {
-    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
-  }
 }
 
 #if SP_X3S_STAMP
@@ -503,10 +499,6 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
-  if (p.splits > 1 && p.flags) {
-    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
-  }
 }
 
 template <int WM, int WN, int TM, int TN, int NS>
@@ -518,23 +510,21 @@ int launch_pipe(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
-  ConvArgs b = a;
-  splitk_flags_fit(b, tiles);
   // NS stages of the fp32 A tile + PL bf16 B planes must fit the 160 KiB LDS
   constexpr bool fits3 = NS * (BM * 8 + 3 * BN * 4) * 16 <= 163840;
   if (planes == 3) {
     if constexpr (fits3) {
-      hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, b);
+      hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 3, NS>), grid, dim3(64 * WM * WN), 0, s, a);
     } else {
       set_error("sp_conv2d: pipe tile %dx%d with %d stages does not fit LDS in f32x3 mode", BM, BN, NS);
       return -1;
     }
   } else {
-    hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, b);
+    hipLaunchKernelGGL((conv_pipe_kernel<WM, WN, TM, TN, 1, NS>), grid, dim3(64 * WM * WN), 0, s, a);
   }
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 pipe)" : "sp_conv2d(bf16 pipe)");
-  if (rc || b.splits == 1 || b.flags) return rc;
-  return launch_splitk_reduce(b, s);
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -736,10 +726,6 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
-  if (p.splits > 1 && p.flags) {
-    __syncthreads();  // every wave done with its slab: smem[0] carries the arrival flag
-    splitk_fixup<NT, BM, BN>(p, blockIdx.x, m0, n0, reinterpret_cast<int*>(smem));
-  }
 }
 
 template <int TM, int TN>
@@ -751,15 +737,13 @@ int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
-  ConvArgs b = a;
-  splitk_flags_fit(b, tiles);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 3>), grid, dim3(512), 0, s, b);
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 3>), grid, dim3(512), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 1>), grid, dim3(512), 0, s, b);
+    hipLaunchKernelGGL((conv_pp_kernel<TM, TN, 1>), grid, dim3(512), 0, s, a);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 ping-pong)" : "sp_conv2d(bf16 ping-pong)");
-  if (rc || b.splits == 1 || b.flags) return rc;
-  return launch_splitk_reduce(b, s);
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
 }
 
 
@@ -1356,15 +1340,13 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
-  ConvArgs b = a;
-  splitk_flags_fit(b, tiles);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, b);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, a);
   else
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, b);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, a);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3)" : "sp_conv2d(bf16)");
-  if (rc || b.splits == 1 || b.flags) return rc;
-  return launch_splitk_reduce(b, s);
+  if (rc || a.splits == 1) return rc;
+  return launch_splitk_reduce(a, s);
 }
 
 }  // namespace
@@ -1401,15 +1383,13 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   if (!a.fast) {  // generic gather: one small-tile instance per operand mode
     const int64_t tiles = ((a.M + 63) / 64) * ((a.d.Cout + 63) / 64);
     dim3 grid((unsigned)tiles, 1, a.splits);
-    ConvArgs b = a;
-    splitk_flags_fit(b, tiles);
     if (planes == 3)
-      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 3, false>), grid, dim3(256), 0, s, b);
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 3, false>), grid, dim3(256), 0, s, a);
     else
-      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 1, false>), grid, dim3(256), 0, s, b);
+      hipLaunchKernelGGL((conv_mfma16_kernel<2, 2, 1, 1, 1, false>), grid, dim3(256), 0, s, a);
     int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3 generic)" : "sp_conv2d(bf16 generic)");
-    if (rc || b.splits == 1 || b.flags) return rc;
-    return launch_splitk_reduce(b, s);
+    if (rc || a.splits == 1) return rc;
+    return launch_splitk_reduce(a, s);
   }
   if (cfg >= 70 && cfg <= 75 && (a.d.C_bf16 || a.d.res1_bf16 || a.d.res2_bf16)) cfg = -1;  // register epilogues: fp32 rows only
   if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1 && a.vec_epi) {
@@ -1452,11 +1432,11 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
     cfg += 100;
   const int gc = cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;  // cfg + 100: the LDS-DMA residual epilogue variant
-  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 68)) && !a.d.A2) {
+  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 68 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

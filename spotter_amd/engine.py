@@ -227,9 +227,6 @@ class Engine:
         # describing the kernels; k > 1 stays available (Engine.forward(microbatches=k) / bench.py
         # --microbatches k)
         self.microbatches = None
-        # split-K GEMMs (bs1) combine their partial sums inside the kernel (ABI v11 splitk_flags) instead of a
-        # separate reduce launch; False keeps the reduce launch (A/B, tools/bs1_ab.py)
-        self.splitk_inkernel = True
         self.stagger = 1  # residual blocks of offset between consecutive micro-batch streams
 
     # ------------------------------------------------------------------ weights
@@ -474,8 +471,7 @@ class Engine:
                               act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm, vpl))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
-                          workspace=self._buf("splitk", self.SPLITK_ELEMS), splitk_flags=self._flags(), **_wkw(cw.w16),
-                          **kw)
+                          workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)
 
     def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None,
                 ln=None):
@@ -494,25 +490,10 @@ class Engine:
         if ln is not None:  # unfused: GEMM into a scratch row block, then sp_layernorm into `out`
             tmp = view(self._buf("ln_tmp", rows, lw.n), lw.n)
             ops.linear(x, rows, lw.k, lw.w, lw.n, tmp, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                       row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), splitk_flags=self._flags(),
-                       **_wkw(lw.w16))
+                       row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
             return ops.layernorm(tmp, *ln, out, rows, lw.n, self.cfg.layer_norm_eps)
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS),
-                          splitk_flags=self._flags(), **_wkw(lw.w16))
-
-    SPLITK_FLAGS = 2048  # split-K arrival counters per context (the split rule keeps grids under 1024 tiles)
-
-    def _flags(self):
-        """The context's zeroed split-K arrival counters (ABI v11 in-kernel combine): every launch leaves
-        them zero, so one tensor serves the whole stream; allocated (and zeroed) outside graph capture."""
-        if not self.splitk_inkernel:
-            return None
-        t = self._ws.get("splitk_flags")
-        if t is None:
-            t = torch.zeros(self.SPLITK_FLAGS, dtype=torch.int32, device=self.dev)
-            self._ws["splitk_flags"] = t
-        return t
+                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
 
     C64_MIN_PIXELS = 1 << 18
     C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)

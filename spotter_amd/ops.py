@@ -79,7 +79,7 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
            wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None,
-           a_bf16=None, splitk_flags: torch.Tensor | None = None):
+           a_bf16=None):
     """ln = (gamma, beta, eps): LayerNorm over each output row fused into the epilogue (fp32 weights).
     a_bf16 = (planes, plane_stride): A as int16 bf16 bit planes with x's row layout (one plane for the
     bf16 operand mode, hi / mid / lo plane_stride elements apart for the split mode) replacing x's fp32
@@ -90,10 +90,7 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     plane count.
     wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
     wt_planes (int16 [3, Cout*K]: the hi / mid / lo bf16 split of the fp32 weights, split_bf16x3)
-    selects the fp32-accurate 3-way-split path (SP_PREC_F32X3).
-    splitk_flags (int32 CUDA tensor, zero, with a workspace; ABI v11): the split-K GEMMs combine their partial
-    sums inside the kernel (last workgroup per tile, fixed z order) instead of a separate reduce launch; the
-    counters are zero again when the launch completes, so one tensor serves every call of a stream."""
+    selects the fp32-accurate 3-way-split path (SP_PREC_F32X3)."""
     ho = (h + 2 * pad - k) // stride + 1
     wo = (w + 2 * pad - k) // stride + 1
     m = n * ho * wo
@@ -181,11 +178,6 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
         d.workspace_elems = workspace.numel()
-        if splitk_flags is not None:
-            if splitk_flags.dtype != torch.int32 or not splitk_flags.is_cuda or not splitk_flags.is_contiguous():
-                raise ValueError("conv: splitk_flags must be a contiguous int32 CUDA tensor")
-            d.splitk_flags = splitk_flags.data_ptr()
-            d.splitk_flags_len = splitk_flags.numel()
     # compulsory bytes: activations at their storage width (fp32 or bf16 rows), weights in the operand form
     # the GEMM streams (fp32, one bf16 plane, or the three split planes)
     wbytes = 2 if wt16 is not None else 6 if wt_planes is not None else 4
@@ -238,10 +230,10 @@ def wino_work_elems(wm: int, tiles: int, cin: int, cout: int, v_planes: bool = F
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
            res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
-           scale=None, workspace=None, wt16=None, wt_planes=None, ln=None, splitk_flags=None):
+           scale=None, workspace=None, wt16=None, wt_planes=None, ln=None):
     return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
                   res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes,
-                  ln=ln, splitk_flags=splitk_flags)
+                  ln=ln)
 
 
 def bf16_bits(a) -> np.ndarray:

@@ -622,7 +622,9 @@ def test_detect_path_harness_with_fake_model():
 
     async def run():
         async with httpx.AsyncClient() as client:
-            return await detect_path.handle(json.dumps({"image_urls": [url]}).encode(), client, Proc(), Model(), {})
+            # no GPU here: the reference's host decode (the GPU path is test_gpu_jpeg.py's)
+            return await detect_path.handle(json.dumps({"image_urls": [url]}).encode(), client, Proc(), Model(), {},
+                                            detect_path.opener("host"))
 
     try:
         out = json.loads(asyncio.run(run()))

@@ -1,7 +1,8 @@
-"""bs1 forward A/B on hipGraph replays: the split-K combine (in-kernel vs the reduce launch) and the tile of
-the split-K launches (sp_set_splitk_config), same process, variants interleaved over several rounds.
+"""bs1 forward A/B on hipGraph replays: the split-K launches' tile, split cap and minimum k-tiles
+(sp_set_splitk_config) and the fused post-LayerNorm epilogue (Engine.fuse_ln), same process, variants
+interleaved over several rounds.
 
-    python tools/bs1_ab.py [--preset r101vd] [--reps 100] [--rounds 3] [--variants reduce:4,inkernel:4,...]
+    python tools/bs1_ab.py [--preset r101vd] [--reps 100] [--rounds 3] [--variants plain:-1:16:8,ln:-1,...]
 
 Prints one JSON line per variant: median replay ms per round, and the max |Δ| of its logits / boxes against
 the first variant (bit-identical expected for the same tile; same-order sums for another tile)."""
@@ -26,8 +27,7 @@ def main():
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="reduce:4:16,inkernel:4:16,reduce:66:16,reduce:67:16,reduce:67:4,"
-                                          "reduce:67:2,reduce:4:1")
+    ap.add_argument("--variants", default="plain:-1:16:8,plain:14:16:8,plain:-1:4:8,plain:-1:16:16,ln:-1:16:8")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = PRESETS[a.preset]
@@ -35,13 +35,12 @@ def main():
     eng = Engine(cfg, generate(cfg, seed=0), dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
-    dflt = ["reduce", "-1", "16", "8"]  # combine : split-K tile : max splits : min k-tiles to split
+    dflt = ["plain", "-1", "16", "8"]  # plain|ln (fused LayerNorm) : split-K tile : max splits : min k-tiles
     variants = [(lambda q: q + dflt[len(q):])(v.split(":")) for v in a.variants.split(",")]
     runners, ref = {}, None
     res = {}
     for mode, c, ms, mk in variants:
-        eng.splitk_inkernel = mode.startswith("inkernel")
-        eng.fuse_ln = mode.endswith("ln")  # "reduce_ln" / "inkernel_ln": post-LNs fused into the GEMM epilogue
+        eng.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
         ops.force_splitk_config(c, int(ms), int(mk))
         try:
             r = GraphRunner(eng, 1, cfg.image_size, cfg.image_size)
