@@ -96,16 +96,10 @@ typedef struct {
   const float* ln_gamma;
   const float* ln_beta;
   float ln_eps;
-  /* ABI v10: operands written as bf16 planes by their producer.
-   * A_bf16 (non-NULL) replaces A for sp_conv2d's LDS-DMA tiles: one bf16 plane (SP_PREC_BF16) or the
-   * hi / mid / lo planes of the split (SP_PREC_F32X3, a_plane_stride elements apart) — the GEMM then
-   * stages them as they are instead of rounding / splitting fp32 A per fragment; lda counts elements.
-   * wino_v_planes (sp_winograd_f43_*, SP_PREC_F32X3): the input transform writes V as its hi / mid /
-   * lo bf16 planes (the exact split the GEMM would compute) and the component GEMM stages them; the
-   * workspace then needs 36 * T * (1.5 * Cin + Cout) floats. Results are bit-identical either way. */
+  /* ABI v10: A_bf16 (non-NULL, SP_PREC_BF16) replaces A for sp_conv2d's LDS-DMA tiles: the activations as
+   * bf16 rows written by their producer (the bf16 variant's maps), staged as they are instead of rounded per
+   * fragment; lda counts elements. */
   const uint16_t* A_bf16;
-  int64_t a_plane_stride;
-  int32_t wino_v_planes;
   /* ABI v10: bf16 activations (the bf16 variant keeps the backbone's maps in bf16). C_bf16 (non-NULL)
    * replaces C: the epilogue result is stored as bf16 (RNE) rows, ldc / out_group_stride in elements.
    * res1_bf16 / res2_bf16 (non-NULL) replace res1 / res2 (bf16 rows, ldr1 / ldr2 in elements). Not with
@@ -212,13 +206,8 @@ int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const float* sca
  * (v_mfma_f32_32x32x2_f32). Direct LDS-halo convolution (RN:78-103). */
 int sp_conv3x3_c32(const float* x, const float* wt, const float* scale, const float* shift, float* y, int n, int h,
                    int w, int cout, int act, void* stream);
-/* The ResNet stage-0 3x3 (Cin 64 → Cout 64, stride 1 pad 1, RN:170-231) in the fp32 modes: fp32 NHWC rows ldx /
- * ldy floats apart (>= 64, % 4, 16-byte aligned: y may be a channel slice of a wider buffer), weights fp32
- * [64][3][3][64], FrozenBN (scale, shift) + act, exact fp32 products (v_mfma_f32_32x32x2_f32). Direct LDS-halo
- * convolution. */
-int sp_conv3x3_c64(const float* x, int64_t ldx, const float* wt, const float* scale, const float* shift, float* y,
-                   int64_t ldy, int n, int h, int w, int act, void* stream);
-/* The same conv on bf16 rows (the bf16 variant): bf16 [64][3][3][64] weights, rows ldx (% 8) / ldy (% 4)
+/* The ResNet stage-0 3x3 (Cin 64 → Cout 64, stride 1 pad 1, RN:170-231) on bf16 rows (the bf16 variant):
+ * bf16 [64][3][3][64] weights, rows ldx (% 8) / ldy (% 4)
  * elements apart, fp32 accumulate, BN (+ the optional pre-activation residual res, bf16 rows ldr apart: the
  * basic block's shortcut, RN:170-200) + act in fp32, RNE at the store. */
 int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_t* w16, const float* scale, const float* shift,

@@ -64,7 +64,8 @@ def make_preprocess():
                         seeds=np.array(rec["seeds"]), digests=np.array(rec["digests"]))
 
 
-def make_model(preset: str, size: int = 640, seeds=(0, 1, -2), with_pic=True, tag=None, src_sizes=None):
+def make_model(preset: str, size: int = 640, seeds=(0, 1, -2), with_pic=True, tag=None, src_sizes=None,
+               cls_shift: float = 0.0):
     import torch
     from PIL import Image
 
@@ -76,6 +77,10 @@ def make_model(preset: str, size: int = 640, seeds=(0, 1, -2), with_pic=True, ta
     torch.manual_seed(0)
     cfg = PRESETS[preset]
     w = generate(cfg, seed=0)
+    if cls_shift:
+        from spotter_amd.weights import shift_class_bias
+
+        w = shift_class_bias(w, cls_shift)
     model = build_hf_model(cfg, w)
     pp = build_hf_processor()
     pp.size = {"height": size, "width": size}
@@ -86,7 +91,7 @@ def make_model(preset: str, size: int = 640, seeds=(0, 1, -2), with_pic=True, ta
         imgs.append(load_test_pic())
         src_sizes.append(imgs[-1].shape[:2])
     out = {"seeds": np.array(list(seeds) + ([-1] if with_pic else [])), "size": size,
-           "src_sizes": np.array(src_sizes)}
+           "src_sizes": np.array(src_sizes), "cls_bias_shift": np.float32(cls_shift)}
     hooks = {}
     model.model.enc_score_head.register_forward_hook(
         lambda m, i, o: hooks.__setitem__("enc_cls", o.detach().numpy()))
@@ -131,8 +136,10 @@ def main(argv):
     if "r101vd_1280" in what:
         # C5: mixed-resolution stream resized on the GPU to 1280²
         # (D1.3 stream sizes; the 717x1200 one is the fixture picture itself)
+        # class biases +1.0 (shift_class_bias): 42-221 detections per image instead of 1-25 at the 640²
+        # bias, so the 1280² parity pins the threshold behaviour on every source size
         make_model("r101vd", size=1280, seeds=(0, 1, 2, 3, 4), with_pic=True, tag="r101vd_1280",
-                   src_sizes=[(480, 640), (720, 1280), (1080, 1920), (1280, 1280), (2160, 3840)])
+                   src_sizes=[(480, 640), (720, 1280), (1080, 1920), (1280, 1280), (2160, 3840)], cls_shift=1.0)
 
 
 if __name__ == "__main__":

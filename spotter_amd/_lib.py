@@ -42,7 +42,7 @@ class SpConvDesc(C.Structure):
         ("workspace", vp), ("workspace_elems", i64),
         ("precision", i32), ("Wt_bf16", vp), ("wt_plane_stride", i64),
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
-        ("A_bf16", vp), ("a_plane_stride", i64), ("wino_v_planes", i32),
+        ("A_bf16", vp),
         ("C_bf16", vp), ("res1_bf16", vp), ("res2_bf16", vp),
     ]
 
@@ -97,7 +97,6 @@ _SIGS = {
     "sp_stem_conv3x3s2_nchw_bf16": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_conv3x3_c32_bf16": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
     "sp_conv3x3_c32": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, vp]),
-    "sp_conv3x3_c64": (i32, [vp, i64, vp, vp, vp, vp, i64, i32, i32, i32, i32, vp]),
     "sp_conv3x3_c64_bf16": (i32, [vp, i64, vp, vp, vp, vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_upsample2x_nearest": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_layernorm": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),

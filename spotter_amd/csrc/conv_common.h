@@ -31,9 +31,8 @@ struct ConvArgs {
   int32_t batch = 1;
   int32_t tiles_per_batch = 0;
   int64_t bs_a = 0, bs_w = 0, bs_c = 0;
-  // A as bf16 planes (LDS-DMA kernels only): A16 != null replaces d.A — one plane for the bf16 operand
-  // mode, three (hi / mid / lo, a_plane_stride elements apart) for the split mode, written by the
-  // producer instead of split per fragment in the GEMM (lda and bs_a count bf16 elements then).
+  // A as bf16 rows (LDS-DMA kernels, bf16 operand mode only): A16 != null replaces d.A, written by the
+  // producer instead of rounded per fragment in the GEMM (lda and bs_a count bf16 elements then).
   const uint16_t* A16 = nullptr;
   int64_t a_plane_stride = 0;
 };

@@ -332,15 +332,13 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
                "sp_conv2d: wt_plane_stride %lld < Cout*K", (long long)d->wt_plane_stride);
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (d->A_bf16) {
-    SP_ARG_CHECK(planes > 0 && !d->A2 && !d->ln_gamma && d->Cin % BK == 0 && d->lda % 8 == 0 && al16(d->A_bf16) &&
-                     (planes == 1 || (d->a_plane_stride % 8 == 0 && d->a_plane_stride > 0)),
-                 "sp_conv2d: bf16 A planes need the bf16 / split operand mode, Cin %% 32 == 0, lda %% 8 == 0, "
-                 "16-byte aligned planes, no A2 / LayerNorm");
+    SP_ARG_CHECK(planes == 1 && !d->A2 && !d->ln_gamma && d->Cin % BK == 0 && d->lda % 8 == 0 && al16(d->A_bf16),
+                 "sp_conv2d: bf16 A rows need the bf16 operand mode, Cin %% 32 == 0, lda %% 8 == 0, 16-byte "
+                 "alignment, no A2 / LayerNorm");
   }
   ConvArgs a;
   a.d = *d;
   a.A16 = d->A_bf16;
-  a.a_plane_stride = d->a_plane_stride;
   a.M = (int64_t)d->N * ho * wo;
   a.K = (int32_t)K;
   a.HoWo = ho * wo;

@@ -37,15 +37,13 @@ namespace {
 
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, int APL = 0>
 struct GldsCfg {
-  // BK = 64 (4 k16 steps per barrier) is supported and was measured: 0.70-0.92x of the same wave tile at
-  // k32 for both operand modes (profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per
-  // CU), so no configuration uses it
-  static_assert(BK == 64 || BK == 32 || BK == 16, "k per stage");
-  static_assert(BK != 64 || 64 * WM * WN >= 256, "64-deep stages: the source swizzle needs >= 256 threads");
+  // (64-deep stages were built and measured at 0.70-0.92x of the same wave tile at k32 for both operand
+  // modes, profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per CU; removed in round 4)
+  static_assert(BK == 32 || BK == 16, "k per stage");
   static constexpr int NT = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
-  // APL: A planes in memory — 0: fp32 A, split per fragment; 1 / 3: bf16 planes (ConvArgs::A16)
+  // APL: A in memory — 0: fp32 A, split / rounded per fragment; 1: bf16 rows (ConvArgs::A16, bf16 mode)
   static_assert(APL == 0 || APL == PL, "bf16 A planes match the operand mode");
   static constexpr int RA = APL ? BK / 8 : BK / 4;  // 16-byte chunks per A row of one plane
   static constexpr int RB = BK / 8;  // 16-byte chunks per bf16 B row (4 / 2)
@@ -96,17 +94,13 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 
   // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
   // (sw16), (row >> 3) & 1 at BK = 16.
-  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
-  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
-                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
+  const int cbk = BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
   // A pieces (per plane): piece j of this thread covers tile row (j·NT + tid) / RA, LDS position
   // tid % RA, global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of
   // the swizzle period. fp32 A: swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way
-  // the 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots;
-  // BK = 64: an A row is 16 chunks = one whole 256-byte bank row, swizzle row & 15. bf16 A planes: the
-  // B rows' swizzle.
+  // the 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
+  // bf16 A rows: the B rows' swizzle.
   const int ca = APL ? cbk
-               : BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
                : BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
   const char* A = (APL ? reinterpret_cast<const char*>(p.A16) : reinterpret_cast<const char*>(d.A)) +
                   (int64_t)bi * p.bs_a * ES;
@@ -255,9 +249,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int brow = wn * TN * 32 + j * 32 + r;
-        const int bpos = BK == 64   ? brow * 8 + ((2 * s + h) ^ ((brow >> 1) & 7))
-                         : BK == 32 ? sw16(brow, 2 * s + h)
-                                    : brow * 2 + (h ^ ((brow >> 3) & 1));
+        const int bpos = BK == 32 ? sw16(brow, 2 * s + h) : brow * 2 + (h ^ ((brow >> 3) & 1));
 #pragma unroll
         for (int pl = 0; pl < PL; ++pl)
           fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
@@ -267,13 +259,11 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
         const int row = wm * TM * 32 + i * 32 + r;
         bf16x8 fa[PL];
         if constexpr (APL) {
-          const int apos = BK == 64   ? row * 8 + ((2 * s + h) ^ ((row >> 1) & 7))
-                           : BK == 32 ? sw16(row, 2 * s + h)
-                                      : row * 2 + (h ^ ((row >> 3) & 1));
+          const int apos = BK == 32 ? sw16(row, 2 * s + h) : row * 2 + (h ^ ((row >> 3) & 1));
 #pragma unroll
           for (int pl = 0; pl < PL; ++pl) fa[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CAP + apos);
         } else {
-        const int sz = BK == 64 ? row & 15 : BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
+        const int sz = BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
         const int c0 = 4 * s + 2 * h;
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
@@ -594,13 +584,12 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   // a tile whose stages do not fit the 160 KB LDS for this operand mode is not instantiated
   using C3 = GldsCfg<WM, WN, TM, TN, 3, NS, BK>;
   using C1 = GldsCfg<WM, WN, TM, TN, 1, NS, BK>;
-  using C3a = GldsCfg<WM, WN, TM, TN, 3, NS, BK, 3>;
   using C1a = GldsCfg<WM, WN, TM, TN, 1, NS, BK, 1>;
   constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
-  constexpr bool fit3a = AB && C3a::SMEM * 16 <= 163840, fit1a = AB && C1a::SMEM * 16 <= 163840;
+  constexpr bool fit1a = AB && C1a::SMEM * 16 <= 163840;  // bf16 A rows: the bf16 operand mode only
   const bool a16 = a.A16 != nullptr;
-  if (a16 && !(planes == 3 ? fit3a : fit1a)) return -2;  // no bf16-A form of this tile: the caller picks another
-  if ((planes == 3 && !(a16 ? fit3a : fit3)) || (planes != 3 && !(a16 ? fit1a : fit1))) {
+  if (a16 && (planes == 3 || !fit1a)) return -2;  // no bf16-A form of this tile: the caller picks another
+  if ((planes == 3 && !fit3) || (planes != 3 && !(a16 ? fit1a : fit1))) {
     set_error("sp_conv2d: tile configuration not built for %d operand plane(s)%s (LDS or bf16-A variant)", planes,
               a16 ? " with bf16 A planes" : "");
     return -1;
@@ -634,12 +623,6 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 2, OCC>), grid, blk, 0, s, ab);
     else if (planes != 3 && !a16)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 1, NS, BK, M16, 1>), grid, blk, 0, s, ab);
-  }
-  if constexpr (fit3a) {
-    if (planes == 3 && a16 && t1)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 3>), grid, blk, 0, s, ab);
-    else if (planes == 3 && a16)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 1, 1, 3>), grid, blk, 0, s, ab);
   }
   if constexpr (fit1a) {
     if (planes != 3 && a16 && t1 && epv == 3)

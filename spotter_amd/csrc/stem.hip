@@ -490,147 +490,6 @@ extern "C" int sp_conv3x3_c32(const float* x, const float* wt, const float* scal
 }
 
 // ---------------------------------------------------------------------------------------------
-// The backbone's stage-0 3×3 (Cin 64 → Cout 64, stride 1, RN:170-231 conv2 of the first stage's bottlenecks)
-// in the fp32 modes, the same way: direct LDS-halo convolution on v_mfma_f32_32x32x2_f32. All 9·64·64 fp32
-// weights are 147 KB, so a workgroup owns one 32-channel half of Cout (73.7 KB of weights, loaded once: the
-// persistent grid pins each workgroup to one half) and a tile of 2 rows × 64 pixels with its halo
-// (4 × 66 × 64 fp32 = 67.6 KB); four waves, wave v computes row v >> 1, pixels 32·(v & 1) .. +31, 32
-// channels. LDS rows are 16 chunks of 16 B, swizzled chunk ^ (row & 15). The next tile's halo is fetched
-// into registers during the MFMAs, as above.
-namespace sp {
-namespace {
-
-constexpr int F6_TH = 2, F6_HR = F6_TH + 2, F6_HC = C3_TW + 2;
-constexpr int F6_HALO = F6_HR * F6_HC * 16;   // 16-byte chunks of the halo
-constexpr int F6_WCH = 9 * 32 * 16;           // 16-byte chunks of one Cout half's weights
-constexpr int F6_PF = (F6_HALO + 255) / 256;  // halo chunks per thread
-
-__device__ __forceinline__ int f6_swz(int row, int c) { return c ^ (row & 15); }
-
-__global__ __launch_bounds__(256, 1) void conv3x3_c64_f32_kernel(const float* __restrict__ x,
-                                                                 const float* __restrict__ wt,
-                                                                 const float* __restrict__ scale,
-                                                                 const float* __restrict__ shift,
-                                                                 float* __restrict__ y, int64_t ldx, int64_t ldy,
-                                                                 int nimg, int h, int w, int tiles_x, int tiles_y,
-                                                                 int act) {
-  __shared__ uint4 lds[F6_HALO + F6_WCH];
-  __shared__ float aff[64];
-  uint4* halo = lds;
-  uint4* wl = lds + F6_HALO;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int half = blockIdx.x & 1, nb = gridDim.x >> 1;  // this workgroup's Cout half; workgroups per half
-  // weights: global [64][9 taps][64 ci] fp32 → LDS [tap][n (of this half)][chunk ^ swz(n)]
-  for (int i = tid; i < F6_WCH; i += 256) {
-    const int c = i & 15, tn = i >> 4, n = tn / 9, tap = tn - n * 9;
-    wl[(tap * 32 + n) * 16 + f6_swz(n, c)] =
-        *reinterpret_cast<const uint4*>(wt + ((int64_t)(half * 32 + n) * 9 + tap) * 64 + c * 4);
-  }
-  if (tid < 32) {
-    aff[tid] = scale[half * 32 + tid];
-    aff[32 + tid] = shift[half * 32 + tid];
-  }
-  const int64_t ntiles = (int64_t)nimg * tiles_x * tiles_y;
-  uint4 pf[F6_PF];
-  unsigned okm = 0;
-  auto fetch = [&](int64_t t) {
-    const int tx = (int)(t % tiles_x);
-    t /= tiles_x;
-    const int ty = (int)(t % tiles_y);
-    const int b = (int)(t / tiles_y);
-    const int oy0 = ty * F6_TH, ox0 = tx * C3_TW;
-#pragma unroll
-    for (int k = 0; k < F6_PF; ++k) {
-      const int i = tid + k * 256;
-      const int c = i & 15, rc = i >> 4, r = rc / F6_HC, col = rc - r * F6_HC;
-      const int iy = oy0 - 1 + r, ix = ox0 - 1 + col;
-      const bool ok = i < F6_HALO && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
-      const int64_t off = ok ? (((int64_t)b * h + iy) * w + ix) * ldx + c * 4 : 0;
-      pf[k] = *reinterpret_cast<const uint4*>(x + off);
-      okm = k == 0 ? (unsigned)ok : (okm | ((unsigned)ok << k));
-    }
-  };
-  const int64_t first = blockIdx.x >> 1;
-  if (first < ntiles) fetch(first);
-  const int r = lane & 31, hh = lane >> 5;
-  const int orow = wave >> 1, px0 = (wave & 1) * 32;
-  for (int64_t tile = first; tile < ntiles; tile += nb) {
-    __syncthreads();  // the previous tile's halo reads are done
-#pragma unroll
-    for (int k = 0; k < F6_PF; ++k) {
-      const int i = tid + k * 256;
-      if (i < F6_HALO) {
-        const int c = i & 15, rc = i >> 4, col = rc % F6_HC;
-        halo[rc * 16 + f6_swz(col, c)] = (okm >> k) & 1u ? pf[k] : make_uint4(0u, 0u, 0u, 0u);
-      }
-    }
-    __syncthreads();
-    if (tile + nb < ntiles) fetch(tile + nb);  // overlaps the MFMAs below
-    int64_t t = tile;
-    const int tx = (int)(t % tiles_x);
-    t /= tiles_x;
-    const int ty = (int)(t % tiles_y);
-    const int b = (int)(t / tiles_y);
-    const int oy = ty * F6_TH + orow, ox0 = tx * C3_TW + px0;
-    f32x16_s acc;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int tap = kh * 3 + kw;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int ch = 2 * q + hh;  // chunk: ci 8q + 4hh .. +3
-          const f32x4_s fa = *reinterpret_cast<const f32x4_s*>(wl + (tap * 32 + r) * 16 + f6_swz(r, ch));
-          const int col = px0 + r + kw;
-          const f32x4_s fb =
-              *reinterpret_cast<const f32x4_s*>(halo + ((orow + kh) * F6_HC + col) * 16 + f6_swz(col, ch));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[e], fb[e], acc, 0, 0, 0);
-        }
-      }
-    // lane (pixel r, half hh) holds channels 8g + 4hh .. +3 of this Cout half in acc[4g .. 4g+3]
-    const int ox = ox0 + r;
-    if (oy < h && ox < w) {
-      float* yrow = y + (((int64_t)b * h + oy) * w + ox) * ldy + half * 32;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n0 = 8 * g + 4 * hh;
-        float4 v;
-        float* vv = &v.x;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float u = fmaf(acc[4 * g + e], aff[n0 + e], aff[32 + n0 + e]);
-          vv[e] = act ? fmaxf(u, 0.f) : u;
-        }
-        *reinterpret_cast<float4*>(yrow + n0) = v;
-      }
-    }
-  }  // tiles
-}
-
-}  // namespace
-}  // namespace sp
-
-extern "C" int sp_conv3x3_c64(const float* x, int64_t ldx, const float* wt, const float* scale, const float* shift,
-                              float* y, int64_t ldy, int n, int h, int w, int act, void* stream) {
-  using namespace sp;
-  SP_ARG_CHECK(x && wt && scale && shift && y && n > 0 && h > 0 && w > 0 && (act == 0 || act == 1) &&
-                   ldx >= 64 && ldy >= 64 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
-                   ((uintptr_t)wt & 15) == 0 && ((uintptr_t)y & 15) == 0,
-               "sp_conv3x3_c64: bad args (act none/relu, 16-byte aligned fp32 rows, ld >= 64 and % 4)");
-  const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + F6_TH - 1) / F6_TH;
-  const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
-  // persistent: one workgroup per CU, half of them per Cout half
-  const int64_t per_half = tiles < g_num_cus / 2 ? tiles : g_num_cus / 2;
-  hipLaunchKernelGGL(conv3x3_c64_f32_kernel, dim3((unsigned)(2 * (per_half > 0 ? per_half : 1))), dim3(256), 0,
-                     as_stream(stream), x, wt, scale, shift, y, ldx, ldy, n, h, w, tiles_x, tiles_y, act);
-  return check_launch("sp_conv3x3_c64");
-}
-
-// ---------------------------------------------------------------------------------------------
 // The stage-0 3×3 (Cin 64 → Cout 64) of the bf16 variant on bf16 rows: the Cin-32 kernel above with 64-channel
 // rows (8 chunks of 16 B, swizzled chunk ^ ((row >> 1) & 7)), all 9·64·64 bf16 weights (73.7 KB) and an
 // (8 + 2) × 66 × 64 bf16 halo (84.5 KB) in LDS, eight waves (one output row each), rows ldx / ldy elements

@@ -207,71 +207,6 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
   }
 }
 
-// The F(4×4) input transform writing V as the split GEMM's operand planes (sp_conv_desc.wino_v_planes):
-// the same V values (same fma order as wino_in_f43_kernel), each rounded to hi = bf16(v), mid =
-// bf16(v - hi), lo = bf16(v - hi - mid) (RNE) — the exact split the GEMM applies per fragment
-// (split_frag_pk) — into three bf16 planes plane_stride elements apart. Two channels per thread: one
-// 4-byte store per plane and component (a wave stores 256 contiguous bytes).
-__global__ __launch_bounds__(256) void wino_in_f43_planes_kernel(const float* __restrict__ x, int64_t lda, int h,
-                                                                 int w, int cvn, int th, int tw, int64_t T,
-                                                                 uint32_t* __restrict__ V, int64_t cin,
-                                                                 int64_t plane_stride) {
-  typedef typename VT<2>::type vf;
-  const int64_t total = T * cvn;
-  const int64_t plane = T * cin;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = g / cvn;
-    const int c = (int)(g - t * cvn) * 2;
-    const int64_t b = t / ((int64_t)th * tw);
-    const int r = (int)(t - b * th * tw);
-    const int ty = r / tw;
-    const int tx = r - ty * tw;
-    const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
-    vf q[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      vf dr[6];
-      const int yy = y0 + i;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int xx = x0 + j;
-        dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
-                    : vf(0.f);
-      }
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb) {
-        vf acc = vf(0.f);
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          if (kBT43[bb][j] != 0.f) acc = __builtin_elementwise_fma(vf(kBT43[bb][j]), dr[j], acc);
-        q[i][bb] = acc;
-      }
-    }
-    // element offset (t·cin + c) is even: one uint32 = the bf16 pair of channels c, c + 1
-    uint32_t* dst = V + (t * cin + c) / 2;
-#pragma unroll
-    for (int bb = 0; bb < 6; ++bb)
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        vf v = vf(0.f);
-#pragma unroll
-        for (int i = 0; i < 6; ++i)
-          if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
-        const uint32_t hi = cvt_pk_bf16(v.x, v.y);
-        const float ra = v.x - __builtin_bit_cast(float, hi << 16);
-        const float rb = v.y - __builtin_bit_cast(float, hi & 0xffff0000u);
-        const uint32_t mid = cvt_pk_bf16(ra, rb);
-        const uint32_t lo = cvt_pk_bf16(ra - __builtin_bit_cast(float, mid << 16),
-                                        rb - __builtin_bit_cast(float, mid & 0xffff0000u));
-        uint32_t* o = dst + (a * 6 + bb) * plane / 2;
-        o[0] = hi;
-        o[plane_stride / 2] = mid;
-        o[plane_stride] = lo;
-      }
-  }
-}
-
 template <int VW>
 __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restrict__ Mc, int64_t T, int cvn,
                                                            int th, int tw, const sp_conv_desc d) {
@@ -374,14 +309,8 @@ namespace {
 // Validation shared by the Winograd entry points (output tiles MT × MT: 2 for F(2×2,3×3), 4 for
 // F(4×4,3×3); NC = (MT + 2)² components); fills th, tw, T. wt_wino may be null (the transform stages
 // do not read it).
-// V as the split GEMM's bf16 operand planes (sp_conv_desc.wino_v_planes): F(4×4) in the split mode only.
-bool wino_vpl(int mt, const sp_conv_desc* d) { return mt == 4 && d->wino_v_planes && d->precision == SP_PREC_F32X3; }
-
-// Floats of the workspace that V occupies (M follows): NC·T·Cin fp32, or three bf16 planes of that size.
-int64_t wino_v_floats(int nc, int64_t T, int cin, bool vpl) {
-  const int64_t v = (int64_t)nc * T * cin;
-  return vpl ? v / 2 * 3 : v;  // Cin % 32 == 0: v is even and v / 2 · 3 stays a multiple of 4 floats
-}
+// Floats of the workspace that V occupies (M follows): NC·T·Cin fp32.
+int64_t wino_v_floats(int nc, int64_t T, int cin) { return (int64_t)nc * T * cin; }
 
 template <int MT>
 int wino_check(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, int64_t wino_plane_stride,
@@ -412,7 +341,7 @@ int wino_check(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino,
   *tw = (d->W + MT - 1) / MT;
   *T = (int64_t)d->N * *th * *tw;
   SP_ARG_CHECK(*T < 0x7fffffff, "%s: %lld tiles", what, (long long)*T);
-  const int64_t need = wino_v_floats(NC, *T, d->Cin, wino_vpl(MT, d)) + (int64_t)NC * *T * d->Cout;
+  const int64_t need = wino_v_floats(NC, *T, d->Cin) + (int64_t)NC * *T * d->Cout;
   SP_ARG_CHECK(work_elems >= need, "%s: workspace %lld < %lld elements", what, (long long)work_elems,
                (long long)need);
   return 0;
@@ -429,11 +358,6 @@ int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t wor
     const int64_t pairs = (int64_t)d->N * th * ((tw + 1) / 2);
     hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream),
                        d->A, d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
-  } else if (wino_vpl(MT, d)) {
-    const int64_t vplane = (int64_t)NC * T * d->Cin;
-    hipLaunchKernelGGL(wino_in_f43_planes_kernel, dim3(stream_grid(T * d->Cin / 2)), dim3(256), 0,
-                       as_stream(stream), d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T,
-                       reinterpret_cast<uint32_t*>(work), (int64_t)d->Cin, vplane);
   } else {
     if (wino43_in_vw(T * d->Cin) == 1)
       hipLaunchKernelGGL(wino_in_f43_kernel<1>, dim3(stream_grid(T * d->Cin)), dim3(256), 0, as_stream(stream),
@@ -456,11 +380,8 @@ int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, 
   // the NC component GEMMs as one batched launch: M = T tiles, K = Cin, no epilogue
   ConvArgs g;
   memset(&g.d, 0, sizeof(g.d));
-  const bool vpl = wino_vpl(MT, d);
-  const int64_t voff = wino_v_floats(NC, T, d->Cin, vpl);
-  g.d.A = vpl ? nullptr : work;
-  g.A16 = vpl ? reinterpret_cast<const uint16_t*>(work) : nullptr;
-  g.a_plane_stride = vpl ? (int64_t)NC * T * d->Cin : 0;
+  const int64_t voff = wino_v_floats(NC, T, d->Cin);
+  g.d.A = work;
   g.d.lda = d->Cin;
   g.d.N = 1;
   g.d.H = 1;
@@ -520,14 +441,14 @@ int wino_output(const char* what, const sp_conv_desc* d, const float* work, int6
   if constexpr (MT == 2) {
     const int cout4 = d->Cout / 4;
     hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
-                       work + wino_v_floats(NC, T, d->Cin, false), T, cout4, th, tw, *d);
+                       work + wino_v_floats(NC, T, d->Cin), T, cout4, th, tw, *d);
   } else {
     if (wino43_out_vw() == 1)
       hipLaunchKernelGGL(wino_out_f43_kernel<1>, dim3(stream_grid(T * d->Cout)), dim3(256), 0, as_stream(stream),
-                         work + wino_v_floats(NC, T, d->Cin, wino_vpl(MT, d)), T, d->Cout, th, tw, *d);
+                         work + wino_v_floats(NC, T, d->Cin), T, d->Cout, th, tw, *d);
     else
       hipLaunchKernelGGL(wino_out_f43_kernel<2>, dim3(stream_grid(T * d->Cout / 2)), dim3(256), 0,
-                         as_stream(stream), work + wino_v_floats(NC, T, d->Cin, wino_vpl(MT, d)), T, d->Cout / 2,
+                         as_stream(stream), work + wino_v_floats(NC, T, d->Cin), T, d->Cout / 2,
                        th, tw, *d);
   }
   return check_launch(what);

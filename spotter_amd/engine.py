@@ -150,8 +150,8 @@ class Engine:
 
     def __init__(self, cfg: SpotterConfig, weights: dict, device: str | torch.device = "cuda",
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
-                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4, wino_v_planes: bool = False,
-                 bf16_store: bool | None = None, direct_c32: bool = True, direct_c64: bool = False,
+                 fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4,
+                 bf16_store: bool | None = None, direct_c32: bool = True,
                  direct_c64_bf16: bool = True):
         from ._lib import lib
 
@@ -184,11 +184,6 @@ class Engine:
         if wino_m not in (2, 4):
             raise ValueError("wino_m must be 2 (F(2x2,3x3)) or 4 (F(4x4,3x3))")
         self.wino_m = wino_m
-        # F(4x4) on the split mode with the input transform writing V as the GEMM's hi / mid / lo bf16 planes
-        # (sp_conv_desc.wino_v_planes) instead of fp32 V split again per GEMM fragment: bit-identical
-        # (tests/test_gpu_kernels.py) but 0.70-0.87x on the C2 shapes (profiles/r3/x3/ab_wino_v_planes.jsonl:
-        # V grows 1.5x and these short-K GEMMs move as many bytes as they do MFMA work), so off by default
-        self.wino_v_planes = wino_v_planes
         self.precision = precision
         # activations by config (the fused epilogue implements relu / silu / gelu; checkpoint.py refuses others)
         self.act_bb = cfg.hidden_act
@@ -205,8 +200,7 @@ class Engine:
         # the Cin-32 stem 3x3s on fp32-MFMA weights as the direct LDS-halo kernel (sp_conv3x3_c32) instead of
         # the fp32-MFMA implicit GEMM
         self.direct_c32 = direct_c32
-        self.direct_c64 = direct_c64  # the stage-0 3x3 (Cin 64 -> 64) likewise (sp_conv3x3_c64)
-        self.direct_c64_bf16 = direct_c64_bf16  # and on bf16 rows (sp_conv3x3_c64_bf16)
+        self.direct_c64_bf16 = direct_c64_bf16  # the stage-0 3x3 (Cin 64 -> 64) on bf16 rows (sp_conv3x3_c64_bf16)
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -459,16 +453,12 @@ class Engine:
                 # the bf16 variant's stage-0 3x3: direct LDS-halo kernel, bit-identical to the implicit GEMM and
                 # 1.53x it at bs32 / bs256 (814 TF at C3; profiles/r3/bf16/ab_conv3x3_c64_bf16.jsonl)
                 return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act, res1=res1)
-            if self.direct_c64 and res1 is None and not x.is_bf16 and not out.is_bf16 and cw.mode in ("x3", "f32"):
-                # the fp32 modes' form (sp_conv3x3_c64): slower than the split GEMM today, off by default
-                return ops.conv3x3_c64(x, cw.w, cw.scale, cw.shift, out, n, h, w, act=act)
         if cw.wino is not None and stride == 1 and not kw and not x.is_bf16 and self._wino_pays(n * h * w, cw.cin):
             wm = self.wino_m
             tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
-            vpl = self.wino_v_planes and wm == 4 and cw.wino.shape[0] == 3
-            work = self._buf("wino_work", ops.wino_work_elems(wm, tiles, cw.cin, cw.cout, vpl))
+            work = self._buf("wino_work", ops.wino_work_elems(wm, tiles, cw.cin, cw.cout))
             return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, 3, 1, 1, out, scale=cw.scale, shift=cw.shift,
-                              act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm, vpl))
+                              act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
                           workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)

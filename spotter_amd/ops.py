@@ -78,12 +78,8 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
-           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None,
-           a_bf16=None):
+           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None):
     """ln = (gamma, beta, eps): LayerNorm over each output row fused into the epilogue (fp32 weights).
-    a_bf16 = (planes, plane_stride): A as int16 bf16 bit planes with x's row layout (one plane for the
-    bf16 operand mode, hi / mid / lo plane_stride elements apart for the split mode) replacing x's fp32
-    values in the GEMM (sp_conv_desc.A_bf16, ABI v10).
     wino = (planes, work[, m]): run this 3×3 stride-1 conv as Winograd F(m×m, 3×3), m = 2 (default) or 4
     (sp_winograd_f23_* / _f43_*), on the transformed weight planes (int16 [3 or 1, (m+2)²·Cout·Cin],
     winograd_weights_host + split) with the fp32 scratch `work`; the bf16 / split operand mode follows the
@@ -100,12 +96,6 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     else:
         d.A = x.need(n * h * w, cin, "conv.A")
     d.lda = x.ld
-    if a_bf16 is not None:
-        a16, aps = a_bf16
-        if a16.dtype != torch.int16 or not a16.is_cuda or not a16.is_contiguous():
-            raise ValueError("conv: bf16 A planes must be a contiguous int16 CUDA tensor")
-        d.A_bf16 = a16.data_ptr()
-        d.a_plane_stride = int(aps)
     if a2 is not None:
         d.A2 = a2.need(n * h * w, cin, "conv.A2")
         d.lda2 = a2.ld
@@ -187,7 +177,6 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     if wino is not None:
         planes, work = wino[0], wino[1]
         wm = wino[2] if len(wino) > 2 else 2
-        vpl = bool(wino[3]) if len(wino) > 3 else False
         nc = (wm + 2) ** 2
         if k != 3 or stride != 1 or pad != 1 or ln is not None or a2 is not None:
             raise ValueError("conv: Winograd needs a 3x3 stride-1 pad-1 conv without A2 / LayerNorm")
@@ -197,11 +186,9 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
                 or planes.dtype != torch.int16 or not planes.is_contiguous() or not planes.is_cuda):
             raise ValueError(f"conv: Winograd weight planes must be int16 [1 or 3, {nc}*Cout*Cin]")
         tiles = n * ((h + wm - 1) // wm) * ((w + wm - 1) // wm)
-        vpl = vpl and wm == 4 and planes.shape[0] == 3
-        if work.dtype != torch.float32 or not work.is_cuda or work.numel() < wino_work_elems(wm, tiles, cin, cout, vpl):
+        if work.dtype != torch.float32 or not work.is_cuda or work.numel() < wino_work_elems(wm, tiles, cin, cout):
             raise ValueError("conv: Winograd workspace too small")
         d.precision = 2 if planes.shape[0] == 3 else 1
-        d.wino_v_planes = int(vpl)
         d.Wt_bf16 = None
         # three launches (sp_winograd_f23_input / _gemm / _output) so the launch hook times the component
         # GEMM, a batched 1x1 GEMM of 16·T rows in the conv's operand mode, apart from the transforms
@@ -220,12 +207,10 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
     return ho, wo
 
 
-def wino_work_elems(wm: int, tiles: int, cin: int, cout: int, v_planes: bool = False) -> int:
-    """fp32 workspace of one Winograd F(wm×wm, 3×3) conv (winograd.hip): V then M; with v_planes V is the
-    split GEMM's three bf16 operand planes (1.5× the fp32 V)."""
+def wino_work_elems(wm: int, tiles: int, cin: int, cout: int) -> int:
+    """fp32 workspace of one Winograd F(wm×wm, 3×3) conv (winograd.hip): V then M."""
     nc = (wm + 2) ** 2
-    v = nc * tiles * cin
-    return (v // 2 * 3 if v_planes else v) + nc * tiles * cout
+    return nc * tiles * (cin + cout)
 
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
@@ -364,22 +349,6 @@ def conv3x3_c32(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor
     _launch("conv", "sp_conv3x3_c32", (xp, wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, n, h, w, cout,
                                        ACT[act], stream()),
             2 * m * cout * 288, 4 * (m * 32 + cout * 288 + m * cout), (m, cout, 288, 3, 1, "f32-direct"))
-
-
-def conv3x3_c64(x: V, wt: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int, w: int,
-                act=None):
-    """The ResNet stage-0 3×3 in the fp32 modes (RN:170-231: 3×3/1, Cin 64 → Cout 64, FrozenBN, act) on fp32 NHWC
-    rows (x and y may be channel slices of wider buffers): the direct LDS-halo kernel sp_conv3x3_c64."""
-    if x.is_bf16 or y.is_bf16 or x.ld % 4 or y.ld % 4 or x.off % 4 or y.off % 4:
-        raise ValueError("conv3x3_c64: 16-byte aligned fp32 row views expected")
-    if wt.dtype != torch.float32 or wt.numel() != 64 * 576 or scale.numel() < 64 or shift.numel() < 64:
-        raise ValueError("conv3x3_c64: weight / affine size mismatch")
-    m = n * h * w
-    xp = x.need(m, 64, "c64.x")
-    yp = y.need(m, 64, "c64.y")
-    _launch("conv", "sp_conv3x3_c64", (xp, x.ld, wt.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, y.ld, n, h,
-                                       w, ACT[act], stream()),
-            2 * m * 64 * 576, 4 * (m * 64 + 64 * 576 + m * 64), (m, 64, 576, 3, 1, "f32-direct"))
 
 
 def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.Tensor, y: V, n: int, h: int,

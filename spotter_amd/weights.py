@@ -265,3 +265,15 @@ def num_params(cfg: SpotterConfig) -> int:
             continue
         n += int(np.prod(shape))
     return n
+
+
+def shift_class_bias(weights: dict, delta: float) -> dict:
+    """A copy of `weights` with every class-head bias (enc_score_head and each decoder class_embed) moved by
+    `delta`: all class logits shift alike, so the encoder's top-300 query selection is unchanged and only
+    how many scores clear the 0.5 threshold moves (used by the 1280² goldens, whose score distribution sits
+    lower than at 640²: tests/golden/r101vd_1280.npz stores the shift it was made with)."""
+    out = dict(weights)
+    for k in weights:
+        if k.endswith(".bias") and (k.startswith("model.enc_score_head") or ".class_embed." in k):
+            out[k] = (weights[k] + np.float32(delta)).astype(np.float32)
+    return out

@@ -346,85 +346,40 @@ def test_winograd_epilogue_views_and_bf16(dev, wm):
     assert np.abs(d16).max() <= 0.05 * np.abs(plain.cpu().numpy()).max(), np.abs(d16).max()
 
 
-@pytest.mark.parametrize("case", WINO_CASES + [(2, 13, 40, 128, 160, "relu")])
-@pytest.mark.parametrize("cfg", [None, "46", "47", "44", "14", "33"])
-def test_winograd_v_planes_bit_identical(dev, case, cfg):
-    """F(4×4) with the input transform writing V as the split GEMM's hi / mid / lo bf16 planes
-    (sp_conv_desc.wino_v_planes, ABI v10) gives exactly the fp32-V result: the transform rounds the same V
-    values the GEMM would split per fragment, and the GEMM stages the planes as they are. With BN, res1,
-    an input channel slice (lda > Cin) and an output slice (ldc > Cout)."""
-    from spotter_amd import ops
-    from spotter_amd.ops import V
-
-    n, h, w, cin, cout, act = case
-    rng = np.random.default_rng(seed(case, 17))
-    m = n * h * w
-    big = rng.standard_normal((m, cin + 32)).astype(np.float32)
-    wt = (rng.standard_normal((cout, 3, 3, cin)) / np.sqrt(9 * cin)).astype(np.float32)
-    kw = dict(scale=T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev),
-              shift=T(rng.standard_normal(cout).astype(np.float32), dev), act=act,
-              res1=V(T(rng.standard_normal(m * cout).astype(np.float32), dev), 0, cout))
-    xd = V(T(big.reshape(-1), dev), 32, cin + 32)
-    wk = T(wt.reshape(cout, -1), dev)
-    planes = T(ops.split_bf16x3_host(ops.winograd_weights_host(wt, 4)), dev)
-    tiles = n * ((h + 3) // 4) * ((w + 3) // 4)
-    outs = []
-    for vpl in (False, True):
-        work = torch.full((ops.wino_work_elems(4, tiles, cin, cout, vpl),), float("nan"), device=dev)
-        out = torch.full((m * (cout + 8),), -7.0, device=dev)
-        ops.force_conv_config(cfg)
-        try:
-            ops.conv2d(xd, n, h, w, cin, wk, cout, 3, 1, 1, V(out, 8, cout + 8), wino=(planes, work, 4, vpl), **kw)
-        except RuntimeError as e:  # a forced tile that cannot take this shape / operand form
-            ops.force_conv_config(None)
-            pytest.skip(str(e))
-        ops.force_conv_config(None)
-        outs.append(out.cpu().numpy())
-    assert not np.isnan(outs[1]).any()
-    assert np.array_equal(outs[0], outs[1]), np.abs(outs[0] - outs[1]).max()
-
-
-def test_conv2d_bf16_a_planes_bit_identical(dev):
-    """sp_conv2d with A given as bf16 planes (sp_conv_desc.A_bf16, ABI v10) equals the fp32-A launch when
-    the planes hold the exact split (x3) / rounding (bf16) of that fp32 A: 1×1 and 3×3 stride-2 convs,
-    ragged M / Cout, residual epilogue, every LDS-DMA tile that builds the bf16-A form."""
+def test_conv2d_bf16_a_rows_bit_identical(dev):
+    """sp_conv2d with A given as bf16 rows (sp_conv_desc.A_bf16, the bf16 variant's maps) equals the launch on
+    the same values as fp32 A (rounded to bf16 per fragment inside the GEMM, exactly): 1×1 and 3×3 stride-2
+    convs, ragged M / Cout, residual epilogue, every LDS-DMA tile that builds the bf16-A form."""
     from spotter_amd import ops
     from spotter_amd.ops import V
 
     rng = np.random.default_rng(23)
     for (n, h, w, cin, cout, k, stride) in [(2, 9, 13, 64, 96, 1, 1), (1, 17, 15, 32, 72, 3, 2),
                                              (3, 8, 8, 128, 256, 3, 1)]:
-        x = rng.standard_normal((n * h * w, cin)).astype(np.float32)
+        x16, xf = _bf16_rows(rng.standard_normal((n * h * w, cin)).astype(np.float32))
         wt = (rng.standard_normal((cout, k * k * cin)) / np.sqrt(k * k * cin)).astype(np.float32)
         ho, wo = (h + 2 * (k // 2) - k) // stride + 1, (w + 2 * (k // 2) - k) // stride + 1
         res = rng.standard_normal((n * ho * wo, cout)).astype(np.float32)
         wk = T(wt, dev)
-        xs = ops.split_bf16x3_host(x)  # [3, rows·cin] hi / mid / lo
-        for mode in ("x3", "bf16"):
-            pl = xs if mode == "x3" else xs[:1]
-            a16 = T(np.ascontiguousarray(pl).reshape(-1).view(np.int16), dev)
-            wkw = dict(wt_planes=ops.split_bf16x3(wk)) if mode == "x3" else dict(
-                wt16=T(ops.bf16_bits(wt).view(np.int16), dev))
-            for cfg in (None, "14", "46", "45", "12", "33", "47", "63", "16", "51", "41", "44", "64", "13"):  # (42: no split-A-plane form fits the LDS)
-                outs = []
-                for use16 in (False, True):
-                    out = torch.full((n * ho * wo * cout,), float("nan"), device=dev)
-                    xin = T(x.reshape(-1), dev) if mode == "x3" else T(ops._bf16_float(xs[0]).reshape(-1), dev)
-                    ops.force_conv_config(cfg)
-                    try:
-                        ops.conv2d(V(xin, 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2, V(out, 0, cout),
-                                   res1=V(T(res.reshape(-1), dev), 0, cout), act="relu",
-                                   a_bf16=(a16, x.size) if use16 else None, **wkw)
-                    except RuntimeError as e:
-                        ops.force_conv_config(None)
-                        outs.append(str(e))
-                        continue
-                    ops.force_conv_config(None)
-                    outs.append(out.cpu().numpy())
-                if any(isinstance(o, str) for o in outs):
-                    assert cfg is not None, outs  # only a forced tile may lack the form
+        w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
+        for cfg in (None, "14", "46", "45", "12", "33", "47", "63", "16", "51", "41", "44", "64", "13"):
+            outs = []
+            for xin in (T(xf.reshape(-1), dev), T(x16.reshape(-1), dev)):  # fp32 values, then the bf16 rows
+                out = torch.full((n * ho * wo * cout,), float("nan"), device=dev)
+                ops.force_conv_config(cfg)
+                try:
+                    ops.conv2d(V(xin, 0, cin), n, h, w, cin, wk, cout, k, stride, k // 2, V(out, 0, cout),
+                               res1=V(T(res.reshape(-1), dev), 0, cout), act="relu", wt16=w16)
+                except RuntimeError as e:
+                    outs.append(str(e))
                     continue
-                assert np.array_equal(outs[0], outs[1]), (mode, cfg, k, np.abs(outs[0] - outs[1]).max())
+                finally:
+                    ops.force_conv_config(None)
+                outs.append(out.cpu().numpy())
+            if any(isinstance(o, str) for o in outs):
+                assert cfg is not None, outs  # only a forced tile may lack the form
+                continue
+            assert np.array_equal(outs[0], outs[1]), (cfg, k, np.abs(outs[0] - outs[1]).max())
 
 
 def _bf16_rows(a):
@@ -536,49 +491,6 @@ def test_conv3x3_c32_f32_direct(dev, cout, act, hw):
     assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, cout)).max() <= tol
 
 
-@pytest.mark.parametrize("act,hw,lds", [("relu", (13, 70), (64, 64)), (None, (5, 129), (128, 192)),
-                                        ("relu", (1, 1), (64, 128)), ("relu", (40, 64), (64, 64))])
-def test_conv3x3_c64_f32_direct(dev, act, hw, lds):
-    """sp_conv3x3_c64 (the fp32 modes' stage-0 3×3, Cin 64 → 64) against an fp64 conv and the fp32-MFMA
-    implicit GEMM, within 3e-6 of the output scale; input / output as channel slices of wider rows (the fused
-    bottleneck tail's layout), ragged tiles, one-pixel maps, more tiles than workgroups; the columns around
-    the output slice stay untouched."""
-    from spotter_amd import ops
-    from spotter_amd.ops import V
-
-    rng = np.random.default_rng(71)
-    n, (h, w) = 2, hw
-    ldx, ldy = lds
-    m = n * h * w
-    x = rng.standard_normal((n, h, w, 64)).astype(np.float32)
-    xrows = np.zeros((m, ldx), np.float32)
-    xrows[:, ldx - 64:] = x.reshape(m, 64)
-    wt = (rng.standard_normal((64, 3, 3, 64)) / 24).astype(np.float32)
-    sc, sh = rng.uniform(0.5, 1.5, 64).astype(np.float32), rng.standard_normal(64).astype(np.float32)
-    xd, wd, scd, shd = T(xrows.reshape(-1), dev), T(wt.reshape(64, 576), dev), T(sc, dev), T(sh, dev)
-    xv = V(xd, ldx - 64, ldx)
-    ref = torch.empty(m * 64, device=dev)
-    ops.conv2d(xv, n, h, w, 64, wd, 64, 3, 1, 1, V(ref, 0, 64), scale=scd, shift=shd, act=act)
-    out = torch.full((m * ldy,), float("nan"), device=dev)
-    yo = ldy - 64
-    ops.conv3x3_c64(xv, wd, scd, shd, V(out, yo, ldy), n, h, w, act=act)
-    rows = out.cpu().numpy().reshape(m, ldy)
-    got = rows[:, yo:].reshape(n, h, w, 64)
-    assert np.isnan(rows[:, :yo]).all()
-    xp = np.pad(x.astype(np.float64), ((0, 0), (1, 1), (1, 1), (0, 0)))
-    acc = np.zeros((n, h, w, 64))
-    for kh in range(3):
-        for kw in range(3):
-            acc += xp[:, kh:kh + h, kw:kw + w, :] @ wt[:, kh, kw, :].astype(np.float64).T
-    want = acc * sc + sh
-    if act:
-        want = np.maximum(want, 0)
-    tol = 3e-6 * np.abs(want).max()
-    assert np.isfinite(got).all()
-    assert np.abs(got - want).max() <= tol
-    assert np.abs(got - ref.cpu().numpy().reshape(n, h, w, 64)).max() <= tol
-
-
 @pytest.mark.parametrize("act,hw,lds,res", [("relu", (13, 70), (64, 64), False), (None, (9, 129), (128, 192), False),
                                             ("relu", (1, 1), (64, 128), False), ("relu", (40, 64), (64, 64), False),
                                             ("relu", (13, 70), (64, 128), True), (None, (9, 129), (128, 64), True)])
@@ -619,6 +531,55 @@ def test_conv3x3_c64_bf16_direct(dev, act, hw, lds, res):
     assert np.all(rows[:, :ldy - 64] == -1)
     assert np.array_equal(rows[:, ldy - 64:], ref.cpu().numpy().reshape(m, 64))
 
+
+
+@pytest.mark.parametrize("kind", ["c32_bf16_32", "c32_bf16_64", "c32_f32_32", "c32_f32_64", "c64_bf16", "c64_bf16_res"])
+def test_direct_3x3_persistent_loop_many_tiles(dev, kind):
+    """The persistent direct 3×3 kernels walk several tiles per workgroup (grid capped near the CU count) and
+    prefetch the next tile's halo during the MFMAs: at n = 8 of 160×160 (480 tiles of 8 rows × 64 pixels per
+    Cout group, well over the grid) every tile after the first comes through that loop. Checked against the
+    implicit GEMM on the same operands: bit for bit on bf16 rows, within 3e-6 of the output scale in fp32."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(91)
+    n, h, w = 8, 160, 160
+    m = n * h * w
+    cin = 64 if kind.startswith("c64") else 32
+    cout = 64 if kind.endswith(("64", "bf16", "res")) else 32
+    wt = (rng.standard_normal((cout, 9 * cin)) / np.sqrt(9 * cin)).astype(np.float32)
+    sc = T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev)
+    sh = T(rng.standard_normal(cout).astype(np.float32), dev)
+    if "f32" in kind:
+        xd = T(rng.standard_normal(m * cin).astype(np.float32), dev)
+        wd = T(wt, dev)
+        ref = torch.empty(m * cout, device=dev)
+        ops.conv2d(V(xd, 0, cin), n, h, w, cin, wd, cout, 3, 1, 1, V(ref, 0, cout), scale=sc, shift=sh, act="relu")
+        out = torch.full((m * cout,), float("nan"), device=dev)
+        ops.conv3x3_c32(V(xd, 0, cin), wd, sc, sh, V(out, 0, cout), n, h, w, cout, act="relu")
+        r, o = ref.cpu().numpy(), out.cpu().numpy()
+        assert np.isfinite(o).all() and np.abs(o - r).max() <= 3e-6 * np.abs(r).max()
+        return
+    x16, _ = _bf16_rows(rng.standard_normal((m, cin)).astype(np.float32))
+    xd = T(x16.reshape(-1), dev)
+    w16 = T(ops.bf16_bits(wt).view(np.int16), dev)
+    rv = None
+    if kind.endswith("res"):
+        r16, _ = _bf16_rows(rng.standard_normal((m, cout)).astype(np.float32))
+        rv = V(T(r16.reshape(-1), dev), 0, cout)
+    ref = torch.full((m * cout,), -1, dtype=torch.int16, device=dev)
+    ops.force_conv_config("14")
+    try:
+        ops.conv2d(V(xd, 0, cin), n, h, w, cin, T(wt, dev), cout, 3, 1, 1, V(ref, 0, cout), scale=sc, shift=sh,
+                   act="relu", wt16=w16, res1=rv)
+    finally:
+        ops.force_conv_config(None)
+    out = torch.full((m * cout,), -1, dtype=torch.int16, device=dev)
+    if cin == 32:
+        ops.conv3x3_c32_bf16(V(xd, 0, cin), w16, sc, sh, V(out, 0, cout), n, h, w, cout, act="relu")
+    else:
+        ops.conv3x3_c64_bf16(V(xd, 0, cin), w16, sc, sh, V(out, 0, cout), n, h, w, act="relu", res1=rv)
+    assert np.array_equal(out.cpu().numpy(), ref.cpu().numpy())
 
 def test_pools_and_stem_bf16_rows(dev):
     """sp_maxpool3x3s2_bf16 / sp_avgpool2x2_ceil_bf16 / sp_stem_conv3x3s2_nchw_bf16 (ABI v10) equal the fp32

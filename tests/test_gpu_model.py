@@ -92,7 +92,12 @@ def run_case(preset, tag=None, precision="fp32", model=None):
     size = int(g["size"])
     # eager: read topk from _ws
     if model is None:
-        model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False, precision=precision)
+        w = None
+        if float(g["cls_bias_shift"]) if "cls_bias_shift" in g.files else 0.0:
+            from spotter_amd.weights import generate, shift_class_bias
+
+            w = shift_class_bias(generate(PRESETS[preset], seed=0), float(g["cls_bias_shift"]))
+        model = SpotterForObjectDetection(PRESETS[preset], weights=w, use_graphs=False, precision=precision)
     proc = SpotterImageProcessor(size={"height": size, "width": size})
     imgs = load_images(g)
     for i, img in enumerate(imgs):
@@ -158,9 +163,14 @@ def test_r101vd_bs32_headline_config_matches_hf_goldens(precision):
         check_image(g, b % 4, dets[b], logits[b], boxes[b], topk[b], case=f"r101vd_640_{precision}_bs32")
 
 
+BF16_R18_RECALL = 0.92      # measured 0.943-0.949 (r3 final trees)
+BF16_R18_P95_DSCORE = 0.03  # measured 0.012-0.014
+
+
 def test_r18vd_bf16_bs256_config_c3():
     """C3: R18vd bf16 at batch 256 (the 4 r18vd goldens tiled ×64). Against the fp32 goldens at the bf16
-    bar (recall >= 0.8 of the fp32 detections at IoU 0.5, p95 |Δscore| <= 0.05), and the batch gives each
+    bar (recall >= 0.92 of the fp32 detections at IoU 0.5 — C4's bar; measured 0.943-0.949 — p95 |Δscore|
+    <= 0.03, measured 0.012-0.014), and the batch gives each
     image what a bs1 call of the same bf16 engine gives (per-query max score: p95 within 0.02, max 0.06: the bf16 delta's own size)."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -171,7 +181,7 @@ def test_r18vd_bf16_bs256_config_c3():
     assert logits.shape == (256, 300, 80)
     st = match_stats(dets, g)
     margins.record("r18vd_640_bf16_bs256", recall_vs_fp32_min=st["recall_vs_fp32"], p95_dscore=st["p95_dscore"])
-    assert st["recall_vs_fp32"] >= 0.8 and st["p95_dscore"] <= 0.05, st
+    assert st["recall_vs_fp32"] >= BF16_R18_RECALL and st["p95_dscore"] <= BF16_R18_P95_DSCORE, st
     # every copy of an image inside the batch is bit-identical (rows never interact)
     for b in range(4, 256):
         assert np.array_equal(logits[b], logits[b % 4]), b

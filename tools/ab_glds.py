@@ -43,15 +43,12 @@ EDGES = [(1, 1, 1000, 256, 192, True, "relu"), (3, 7, 9, 128, 320, False, None),
 
 
 PLANES = 3  # 3 = the fp32-accurate split (x3), 1 = the bf16 operand mode (--planes 1)
-VPL = False  # Winograd V as split bf16 planes (configuration suffix "v")
 BF16_ROWS = False  # --bf16-rows: activations / outputs / residuals as bf16 rows (with --planes 1)
 
 
 def force(c):
-    """Select configuration c ("46", "46v": the same tile with Winograd V planes, "-": none)."""
-    global VPL
-    VPL = c.endswith("v")
-    ops.force_conv_config(c.rstrip("v") or None)
+    """Select configuration c ("46", "-": none)."""
+    ops.force_conv_config(None if c == "-" else c)
 
 
 def make(dev, shape, seed=0):
@@ -75,7 +72,7 @@ def make(dev, shape, seed=0):
         planes = (torch.from_numpy(ops.split_bf16x3_host(u)).to(dev) if PLANES == 3 else
                   torch.from_numpy(ops.bf16_bits(u).reshape(1, -1).view("int16")).to(dev))
         t = n * ((h + 3) // 4) * ((w + 3) // 4)
-        work = torch.empty(ops.wino_work_elems(4, t, cin, cout, True), device=dev)
+        work = torch.empty(ops.wino_work_elems(4, t, cin, cout), device=dev)
         kw["wino"] = (planes, work, 4)
     elif PLANES == 3:
         kw["wt_planes"] = ops.split_bf16x3(wt)
@@ -84,11 +81,8 @@ def make(dev, shape, seed=0):
     act = None if wino else shape[6]
 
     def run():
-        kk = dict(kw)
-        if wino:  # a configuration "<cfg>v" runs the Winograd conv with V as bf16 split planes
-            kk["wino"] = kw["wino"] + (VPL,)
         ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, 1, k // 2, view(out, cout), scale=sc, shift=sh,
-                   act=act, res1=view(res, cout) if res is not None else None, **kk)
+                   act=act, res1=view(res, cout) if res is not None else None, **kw)
 
     flops = 2.0 * n * h * w * cout * cin * (9 if wino else 1)  # direct-equivalent for Winograd
     if wino:
