@@ -152,6 +152,13 @@ int sp_set_conv_config(int cfg);
  * factor of this thread's later launches (max_splits < 1 = the default, 16) and the fewest 32-deep k-tiles a
  * launch needs to split at all (min_ktiles < 1 = the default, 8): bs1 tuning hooks. */
 int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles);
+/* Tuning knobs of this thread's later launches (ABI v11; value -1 = the product default), for same-process
+ * A/B measurements; nothing on the product path calls it. */
+enum sp_tuning_knob {
+  SP_TUNE_WINO43_LAYOUT = 1,  /* F(4x4) workspace: 0 component-major [36][T][C], 1 tile-major [T][36][C] */
+  SP_TUNE_WINO43_IN_ROWS = 2, /* F(4x4) input transform: tile rows walked per thread (1, 2, 4, 8) */
+};
+int sp_set_tuning(int knob, int value);
 
 /* 3x3 stride-1 pad-1 convolution by Winograd F(2x2, 3x3) (ABI v9): the same result contract as
  * sp_conv2d on the same descriptor (KH = KW = 3, stride 1, pad 1; act, scale / shift, res1 / res2 as

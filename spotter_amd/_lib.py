@@ -81,6 +81,7 @@ _SIGS = {
     "sp_conv2d": (i32, [C.POINTER(SpConvDesc), vp]),
     "sp_set_conv_config": (i32, [i32]),
     "sp_set_splitk_config": (i32, [i32, i32, i32]),
+    "sp_set_tuning": (i32, [i32, i32]),
     "sp_conv3x3_winograd": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),
     "sp_winograd_f23_input": (i32, [C.POINTER(SpConvDesc), vp, i64, vp]),
     "sp_winograd_f23_gemm": (i32, [C.POINTER(SpConvDesc), vp, i64, vp, i64, vp]),

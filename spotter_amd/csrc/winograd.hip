@@ -157,13 +157,16 @@ struct VT {
 
 // VW consecutive channels per thread (1 or 2: the launch takes 1 on maps too small to fill the chip
 // with 2-channel threads).
+// V element (component k, tile t, channel c) lives at V[k·cstride + t·tstride + c]: component-major
+// (cstride = T·Cin, tstride = Cin, the default) or tile-major (cstride = Cin, tstride = 36·Cin: the 36
+// components of a tile side by side, so both transforms touch one compact region per tile).
 template <int VW>
 __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
                                                           int cvn, int th, int tw, int64_t T,
-                                                          float* __restrict__ V, int64_t cin) {
+                                                          float* __restrict__ V, int64_t tstride, int64_t cstride) {
   typedef typename VT<VW>::type vf;
   const int64_t total = T * cvn;
-  const int64_t plane = T * cin;
+  const int64_t plane = cstride;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = g / cvn;
     const int c = (int)(g - t * cvn) * VW;
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
         q[i][bb] = acc;
       }
     }
-    float* dst = V + t * cin + c;
+    float* dst = V + t * tstride + c;
 #pragma unroll
     for (int bb = 0; bb < 6; ++bb)
 #pragma unroll
@@ -207,13 +210,84 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
   }
 }
 
+// The same transform walking R vertically adjacent tiles per thread: patch rows 4ty-1 .. 4ty+4 of tile ty
+// and ty+1 share two input rows, so the row pass (q[i][·] depends on input row i only) of the last two rows
+// carries over and each further tile loads 4 rows instead of 6 (input reads 1.5× the map instead of
+// 2.25×). Identical arithmetic per value (same fma order), so V is bit-identical to wino_in_f43_kernel's.
+template <int VW, int R>
+__global__ __launch_bounds__(256) void wino_in_f43_rows_kernel(const float* __restrict__ x, int64_t lda, int h,
+                                                               int w, int cvn, int th, int tw, int nb,
+                                                               float* __restrict__ V, int64_t tstride,
+                                                               int64_t cstride) {
+  typedef typename VT<VW>::type vf;
+  const int thr = (th + R - 1) / R;
+  const int64_t total = (int64_t)nb * thr * tw * cvn;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
+    int64_t rest = g / cvn;
+    const int c = (int)(g - rest * cvn) * VW;
+    const int tx = (int)(rest % tw);
+    rest /= tw;
+    const int tyr = (int)(rest % thr);
+    const int64_t b = rest / thr;
+    const int x0 = 4 * tx - 1;
+    vf q[6][6];
+    auto row_pass = [&](int i, int yy) {
+      vf dr[6];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int xx = x0 + j;
+        dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
+                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
+                    : vf(0.f);
+      }
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) {
+        vf acc = vf(0.f);
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (kBT43[bb][j] != 0.f) acc = __builtin_elementwise_fma(vf(kBT43[bb][j]), dr[j], acc);
+        q[i][bb] = acc;
+      }
+    };
+#pragma unroll 1
+    for (int k = 0; k < R; ++k) {
+      const int ty = tyr * R + k;
+      if (ty >= th) break;
+      const int y0 = 4 * ty - 1;
+      if (k == 0) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) row_pass(i, y0 + i);
+      } else {
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+          q[0][bb] = q[4][bb];
+          q[1][bb] = q[5][bb];
+        }
+#pragma unroll
+        for (int i = 2; i < 6; ++i) row_pass(i, y0 + i);
+      }
+      float* dst = V + ((b * th + ty) * tw + tx) * tstride + c;
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb)
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          vf v = vf(0.f);
+#pragma unroll
+          for (int i = 0; i < 6; ++i)
+            if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
+          *reinterpret_cast<vf*>(dst + (a * 6 + bb) * cstride) = v;
+        }
+    }
+  }
+}
+
 template <int VW>
 __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restrict__ Mc, int64_t T, int cvn,
-                                                           int th, int tw, const sp_conv_desc d) {
+                                                           int th, int tw, const sp_conv_desc d, int64_t tstride,
+                                                           int64_t cstride) {
   typedef typename VT<VW>::type vf;
   const int64_t total = T * cvn;
-  const int64_t cout = d.Cout;
-  const int64_t plane = T * cout;
+  const int64_t plane = cstride;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = g / cvn;
     const int n = (int)(g - t * cvn) * VW;
@@ -221,7 +295,7 @@ __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restri
     const int r = (int)(t - b * th * tw);
     const int ty = r / tw;
     const int tx = r - ty * tw;
-    const float* src = Mc + t * cout + n;
+    const float* src = Mc + t * tstride + n;
     vf s[4][6];  // s[p][bb] = Σ_a Aᵀ[p][a] M[a][bb], accumulated as the rows of M arrive
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -292,6 +366,14 @@ int wino43_out_vw() {
   return f ? f : 1;
 }
 
+// Tuning knobs of the F(4×4) path (sp_set_tuning, per calling thread; -1 = the product default): the
+// workspace layout (0 component-major, 1 tile-major) and the input transform's tile rows per thread
+// (1 = one tile per thread; 2, 4, 8 = wino_in_f43_rows_kernel).
+thread_local int g_wino43_layout = -1;
+thread_local int g_wino43_in_rows = -1;
+int wino43_layout() { return g_wino43_layout >= 0 ? g_wino43_layout : 0; }
+int wino43_in_rows() { return g_wino43_in_rows >= 0 ? g_wino43_in_rows : 1; }
+
 int stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   const int64_t cap = (int64_t)g_num_cus * 16;
@@ -359,12 +441,30 @@ int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t wor
     hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream),
                        d->A, d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
   } else {
-    if (wino43_in_vw(T * d->Cin) == 1)
+    const bool tm = wino43_layout() == 1;
+    const int64_t ts = tm ? (int64_t)NC * d->Cin : d->Cin, cs = tm ? (int64_t)d->Cin : T * d->Cin;
+    const int rows = wino43_in_rows();
+    const int vw = wino43_in_vw(T * d->Cin);
+    if (rows > 1) {
+      const int64_t thr = (th + rows - 1) / rows;
+      const int64_t items = (int64_t)d->N * thr * tw * (d->Cin / vw);
+      const dim3 gr(stream_grid(items));
+#define SP_WINO_ROWS(VW, R)                                                                                         \
+  hipLaunchKernelGGL((wino_in_f43_rows_kernel<VW, R>), gr, dim3(256), 0, as_stream(stream), d->A, d->lda, d->H, d->W, \
+                     d->Cin / VW, th, tw, d->N, work, ts, cs)
+      if (vw == 1) {
+        if (rows == 2) SP_WINO_ROWS(1, 2); else if (rows == 4) SP_WINO_ROWS(1, 4); else SP_WINO_ROWS(1, 8);
+      } else {
+        if (rows == 2) SP_WINO_ROWS(2, 2); else if (rows == 4) SP_WINO_ROWS(2, 4); else SP_WINO_ROWS(2, 8);
+      }
+#undef SP_WINO_ROWS
+    } else if (vw == 1) {
       hipLaunchKernelGGL(wino_in_f43_kernel<1>, dim3(stream_grid(T * d->Cin)), dim3(256), 0, as_stream(stream),
-                         d->A, d->lda, d->H, d->W, d->Cin, th, tw, T, work, (int64_t)d->Cin);
-    else
+                         d->A, d->lda, d->H, d->W, d->Cin, th, tw, T, work, ts, cs);
+    } else {
       hipLaunchKernelGGL(wino_in_f43_kernel<2>, dim3(stream_grid(T * d->Cin / 2)), dim3(256), 0, as_stream(stream),
-                         d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T, work, (int64_t)d->Cin);
+                         d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T, work, ts, cs);
+    }
   }
   return check_launch(what);
 }
@@ -410,6 +510,12 @@ int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, 
   g.bs_a = T * d->Cin;
   g.bs_w = (int64_t)d->Cout * d->Cin;
   g.bs_c = T * d->Cout;
+  if (MT == 4 && wino43_layout() == 1) {  // tile-major V / M: component k of tile t at t·NC·C + k·C
+    g.d.lda = (int64_t)NC * d->Cin;
+    g.d.ldc = (int64_t)NC * d->Cout;
+    g.bs_a = d->Cin;
+    g.bs_c = d->Cout;
+  }
   // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py,
   // profiles/r2/tune_wino_x3.json: bs32 shapes, NC × T rows): 256×128 k16 (cfg 44) for the tallest
   // batches and for the wide ones from 400000 rows (bs32 80²×384: 1.25 vs 1.32 ms on two boxes,
@@ -443,13 +549,14 @@ int wino_output(const char* what, const sp_conv_desc* d, const float* work, int6
     hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
                        work + wino_v_floats(NC, T, d->Cin), T, cout4, th, tw, *d);
   } else {
+    const bool tm = wino43_layout() == 1;
+    const int64_t ts = tm ? (int64_t)NC * d->Cout : d->Cout, cs = tm ? (int64_t)d->Cout : T * d->Cout;
     if (wino43_out_vw() == 1)
       hipLaunchKernelGGL(wino_out_f43_kernel<1>, dim3(stream_grid(T * d->Cout)), dim3(256), 0, as_stream(stream),
-                         work + wino_v_floats(NC, T, d->Cin), T, d->Cout, th, tw, *d);
+                         work + wino_v_floats(NC, T, d->Cin), T, d->Cout, th, tw, *d, ts, cs);
     else
       hipLaunchKernelGGL(wino_out_f43_kernel<2>, dim3(stream_grid(T * d->Cout / 2)), dim3(256), 0,
-                         as_stream(stream), work + wino_v_floats(NC, T, d->Cin), T, d->Cout / 2,
-                       th, tw, *d);
+                         as_stream(stream), work + wino_v_floats(NC, T, d->Cin), T, d->Cout / 2, th, tw, *d, ts, cs);
   }
   return check_launch(what);
 }
@@ -488,4 +595,18 @@ extern "C" int sp_winograd_f43_gemm(const sp_conv_desc* d, const uint16_t* wt_wi
 
 extern "C" int sp_winograd_f43_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
   return sp::wino_output<4>("sp_winograd_f43_output", d, work, work_elems, stream);
+}
+
+extern "C" int sp_set_tuning(int knob, int value) {
+  switch (knob) {
+    case SP_TUNE_WINO43_LAYOUT:
+      sp::g_wino43_layout = value == 0 || value == 1 ? value : -1;
+      return 0;
+    case SP_TUNE_WINO43_IN_ROWS:
+      sp::g_wino43_in_rows = value == 1 || value == 2 || value == 4 || value == 8 ? value : -1;
+      return 0;
+    default:
+      sp::set_error("sp_set_tuning: unknown knob %d", knob);
+      return -1;
+  }
 }

@@ -291,6 +291,16 @@ def force_splitk_config(cfg=None, max_splits=None, min_ktiles=None):
                                0 if min_ktiles is None else int(min_ktiles))
 
 
+TUNE_WINO43_LAYOUT, TUNE_WINO43_IN_ROWS = 1, 2  # include/spotter_hip.h sp_tuning_knob
+
+
+def set_tuning(knob: int, value: int | None):
+    """Tuning tools: set a knob of this thread's later launches (sp_set_tuning); None = the product default."""
+    from ._lib import call
+
+    call("sp_set_tuning", int(knob), -1 if value is None else int(value))
+
+
 def nchw_to_nhwc(x: torch.Tensor, y: torch.Tensor):
     n, c, h, w = x.shape
     assert y.numel() >= x.numel() and x.is_contiguous()
