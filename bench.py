@@ -633,6 +633,10 @@ def main():
             "per_rank": per_rank,
             "roofline": roof, "kernel_classes": classes, "cpu_baseline": cpu, "latency": lat,
         }
+        # vs_baseline stays null: BASELINE.md §1 holds no published number for this metric (the reference
+        # publishes none). The same-run CPU reference ratio is reported beside it.
+        if isinstance(cpu, dict) and cpu.get("value"):
+            line["vs_cpu_baseline"] = round(value / cpu["value"], 1)
         if args.stub_step_ms is not None:
             line["data"] = "STUB: no GPU step (launcher test)"
         print(json.dumps(line), flush=True)

@@ -49,6 +49,10 @@ SHAPES = [
     (1, 40, 40, 256, 256, 3, 1, "relu", False, 22),     # 25 stage3 3x3 bs1
     (1, 40, 40, 1024, 256, 1, 1, "relu", False, 22),    # 26 stage3 reduce bs1
     (1, 40, 40, 256, 1024, 1, 1, "relu", True, 23),     # 27 stage3 expand bs1
+    # C3 (R18vd bs256) basic-block 3x3s
+    (256, 80, 80, 128, 128, 3, 1, "relu", False, 3),    # 28 stage1 3x3 (C3's largest bucket)
+    (256, 160, 160, 64, 64, 3, 1, "relu", False, 4),    # 29 stage0 3x3
+    (256, 40, 40, 256, 256, 3, 1, "relu", False, 3),    # 30 stage2 3x3
 ]
 
 
@@ -60,13 +64,18 @@ def bench_one(dev, shape, prec, cfg, reps, ws=False):
     m = n * ho * wo
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(n * h * w * cin, device=dev, generator=g)
+    rows16 = prec == "bf16rows"  # the bf16 variant's form: bf16 activation rows in and out (A16, C_bf16)
+    b16 = lambda t: t.to(torch.bfloat16).view(torch.int16).contiguous()
     wt = torch.randn(cout * k * k * cin, device=dev, generator=g) * (1.0 / (cin * k * k) ** 0.5)
     sc = torch.rand(cout, device=dev, generator=g) + 0.5
     sh = torch.randn(cout, device=dev, generator=g)
-    out = torch.empty(m * cout, device=dev)
+    out = torch.empty(m * cout, device=dev, dtype=torch.int16 if rows16 else torch.float32)
     r1 = torch.randn(m * cout, device=dev, generator=g) if resid else None
+    if rows16:
+        x = b16(x)
+        r1 = b16(r1) if r1 is not None else None
     kw = {}
-    if prec == "bf16":
+    if prec in ("bf16", "bf16rows"):
         kw["wt16"] = wt.to(torch.bfloat16).view(torch.int16).contiguous()
     elif prec == "f32x3":
         kw["wt_planes"] = ops.split_bf16x3(wt)
