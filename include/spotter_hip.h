@@ -156,7 +156,7 @@ int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles);
  * A/B measurements; nothing on the product path calls it. */
 enum sp_tuning_knob {
   SP_TUNE_WINO43_LAYOUT = 1,  /* F(4x4) workspace: 0 component-major [36][T][C], 1 tile-major [T][36][C] */
-  SP_TUNE_WINO43_IN_ROWS = 2, /* F(4x4) input transform: tile rows walked per thread (1, 2, 4, 8) */
+  SP_TUNE_WINO43_IN_NT = 2,   /* F(4x4) input transform: bit 0 non-temporal map loads, bit 1 non-temporal V stores */
 };
 int sp_set_tuning(int knob, int value);
 

@@ -674,7 +674,13 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(62, 4, 1, 1, 8, 2, 32, false, 1, false)    /* 128×256, 4 waves of 32×256 */ \
   X(63, 8, 1, 1, 4, 2, 32, false, 1, true)    /* 256×128, 8 waves of 32×128 */ \
   X(64, 4, 1, 1, 4, 3, 32, false, 1, true)    /* 128×128, 4 waves of 32×128, 3 stages */ \
-  X(65, 8, 1, 1, 4, 2, 32, true, 1, false)     /* cfg 63 on 16x16x32 MFMAs */
+  X(65, 8, 1, 1, 4, 2, 32, true, 1, false)     /* cfg 63 on 16x16x32 MFMAs */ \
+  /* round 4, bf16-row candidates (deeper DMA pipelines; x3 stages do not fit at 256 rows) */ \
+  X(52, 4, 2, 2, 2, 3, 32, false, 1, true)    /* 256×128, k32 × 3 */ \
+  X(53, 4, 2, 2, 2, 3, 32, true, 1, true)     /* cfg 52 on 16x16x32 MFMAs */ \
+  X(54, 4, 2, 2, 2, 4, 32, true, 1, true)     /* 256×128, k32 × 4, 16x16x32 */ \
+  X(55, 4, 2, 2, 4, 3, 32, true, 1, true)     /* 256×256, k32 × 3, 16x16x32 */ \
+  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path

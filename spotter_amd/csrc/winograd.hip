@@ -160,7 +160,8 @@ struct VT {
 // V element (component k, tile t, channel c) lives at V[k·cstride + t·tstride + c]: component-major
 // (cstride = T·Cin, tstride = Cin, the default) or tile-major (cstride = Cin, tstride = 36·Cin: the 36
 // components of a tile side by side, so both transforms touch one compact region per tile).
-template <int VW>
+// NT: bit 0 non-temporal loads of the map, bit 1 non-temporal stores of V (tuning variants, sp_set_tuning).
+template <int VW, int NT = 0>
 __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
                                                           int cvn, int th, int tw, int64_t T,
                                                           float* __restrict__ V, int64_t tstride, int64_t cstride) {
@@ -183,8 +184,9 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int xx = x0 + j;
+        const vf* src = reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c);
         dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
+                    ? ((NT & 1) ? __builtin_nontemporal_load(src) : *src)
                     : vf(0.f);
       }
 #pragma unroll
@@ -205,79 +207,11 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
 #pragma unroll
         for (int i = 0; i < 6; ++i)
           if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
-        *reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane) = v;
+        if constexpr ((NT & 2) != 0)
+          __builtin_nontemporal_store(v, reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane));
+        else
+          *reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane) = v;
       }
-  }
-}
-
-// The same transform walking R vertically adjacent tiles per thread: patch rows 4ty-1 .. 4ty+4 of tile ty
-// and ty+1 share two input rows, so the row pass (q[i][·] depends on input row i only) of the last two rows
-// carries over and each further tile loads 4 rows instead of 6 (input reads 1.5× the map instead of
-// 2.25×). Identical arithmetic per value (same fma order), so V is bit-identical to wino_in_f43_kernel's.
-template <int VW, int R>
-__global__ __launch_bounds__(256) void wino_in_f43_rows_kernel(const float* __restrict__ x, int64_t lda, int h,
-                                                               int w, int cvn, int th, int tw, int nb,
-                                                               float* __restrict__ V, int64_t tstride,
-                                                               int64_t cstride) {
-  typedef typename VT<VW>::type vf;
-  const int thr = (th + R - 1) / R;
-  const int64_t total = (int64_t)nb * thr * tw * cvn;
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total; g += (int64_t)gridDim.x * blockDim.x) {
-    int64_t rest = g / cvn;
-    const int c = (int)(g - rest * cvn) * VW;
-    const int tx = (int)(rest % tw);
-    rest /= tw;
-    const int tyr = (int)(rest % thr);
-    const int64_t b = rest / thr;
-    const int x0 = 4 * tx - 1;
-    vf q[6][6];
-    auto row_pass = [&](int i, int yy) {
-      vf dr[6];
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int xx = x0 + j;
-        dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
-                    : vf(0.f);
-      }
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb) {
-        vf acc = vf(0.f);
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          if (kBT43[bb][j] != 0.f) acc = __builtin_elementwise_fma(vf(kBT43[bb][j]), dr[j], acc);
-        q[i][bb] = acc;
-      }
-    };
-#pragma unroll 1
-    for (int k = 0; k < R; ++k) {
-      const int ty = tyr * R + k;
-      if (ty >= th) break;
-      const int y0 = 4 * ty - 1;
-      if (k == 0) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) row_pass(i, y0 + i);
-      } else {
-#pragma unroll
-        for (int bb = 0; bb < 6; ++bb) {
-          q[0][bb] = q[4][bb];
-          q[1][bb] = q[5][bb];
-        }
-#pragma unroll
-        for (int i = 2; i < 6; ++i) row_pass(i, y0 + i);
-      }
-      float* dst = V + ((b * th + ty) * tw + tx) * tstride + c;
-#pragma unroll
-      for (int bb = 0; bb < 6; ++bb)
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          vf v = vf(0.f);
-#pragma unroll
-          for (int i = 0; i < 6; ++i)
-            if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
-          *reinterpret_cast<vf*>(dst + (a * 6 + bb) * cstride) = v;
-        }
-    }
   }
 }
 
@@ -367,12 +301,11 @@ int wino43_out_vw() {
 }
 
 // Tuning knobs of the F(4×4) path (sp_set_tuning, per calling thread; -1 = the product default): the
-// workspace layout (0 component-major, 1 tile-major) and the input transform's tile rows per thread
-// (1 = one tile per thread; 2, 4, 8 = wino_in_f43_rows_kernel).
+// workspace layout (0 component-major, 1 tile-major) and the input transform's non-temporal accesses.
 thread_local int g_wino43_layout = -1;
-thread_local int g_wino43_in_rows = -1;
+thread_local int g_wino43_in_nt = -1;
 int wino43_layout() { return g_wino43_layout >= 0 ? g_wino43_layout : 0; }
-int wino43_in_rows() { return g_wino43_in_rows >= 0 ? g_wino43_in_rows : 1; }
+int wino43_in_nt() { return g_wino43_in_nt >= 0 ? g_wino43_in_nt : 0; }
 
 int stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
@@ -443,28 +376,19 @@ int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t wor
   } else {
     const bool tm = wino43_layout() == 1;
     const int64_t ts = tm ? (int64_t)NC * d->Cin : d->Cin, cs = tm ? (int64_t)d->Cin : T * d->Cin;
-    const int rows = wino43_in_rows();
-    const int vw = wino43_in_vw(T * d->Cin);
-    if (rows > 1) {
-      const int64_t thr = (th + rows - 1) / rows;
-      const int64_t items = (int64_t)d->N * thr * tw * (d->Cin / vw);
-      const dim3 gr(stream_grid(items));
-#define SP_WINO_ROWS(VW, R)                                                                                         \
-  hipLaunchKernelGGL((wino_in_f43_rows_kernel<VW, R>), gr, dim3(256), 0, as_stream(stream), d->A, d->lda, d->H, d->W, \
-                     d->Cin / VW, th, tw, d->N, work, ts, cs)
-      if (vw == 1) {
-        if (rows == 2) SP_WINO_ROWS(1, 2); else if (rows == 4) SP_WINO_ROWS(1, 4); else SP_WINO_ROWS(1, 8);
-      } else {
-        if (rows == 2) SP_WINO_ROWS(2, 2); else if (rows == 4) SP_WINO_ROWS(2, 4); else SP_WINO_ROWS(2, 8);
-      }
-#undef SP_WINO_ROWS
-    } else if (vw == 1) {
-      hipLaunchKernelGGL(wino_in_f43_kernel<1>, dim3(stream_grid(T * d->Cin)), dim3(256), 0, as_stream(stream),
-                         d->A, d->lda, d->H, d->W, d->Cin, th, tw, T, work, ts, cs);
+    const int vw = wino43_in_vw(T * d->Cin), nt = wino43_in_nt();
+    const dim3 gr(stream_grid(T * d->Cin / vw));
+#define SP_WINO_IN(VW, NT)                                                                                         \
+  hipLaunchKernelGGL((wino_in_f43_kernel<VW, NT>), gr, dim3(256), 0, as_stream(stream), d->A, d->lda, d->H, d->W,  \
+                     d->Cin / VW, th, tw, T, work, ts, cs)
+    if (vw == 1) {
+      if (nt == 1) SP_WINO_IN(1, 1); else if (nt == 2) SP_WINO_IN(1, 2); else if (nt == 3) SP_WINO_IN(1, 3);
+      else SP_WINO_IN(1, 0);
     } else {
-      hipLaunchKernelGGL(wino_in_f43_kernel<2>, dim3(stream_grid(T * d->Cin / 2)), dim3(256), 0, as_stream(stream),
-                         d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T, work, ts, cs);
+      if (nt == 1) SP_WINO_IN(2, 1); else if (nt == 2) SP_WINO_IN(2, 2); else if (nt == 3) SP_WINO_IN(2, 3);
+      else SP_WINO_IN(2, 0);
     }
+#undef SP_WINO_IN
   }
   return check_launch(what);
 }
@@ -602,8 +526,8 @@ extern "C" int sp_set_tuning(int knob, int value) {
     case SP_TUNE_WINO43_LAYOUT:
       sp::g_wino43_layout = value == 0 || value == 1 ? value : -1;
       return 0;
-    case SP_TUNE_WINO43_IN_ROWS:
-      sp::g_wino43_in_rows = value == 1 || value == 2 || value == 4 || value == 8 ? value : -1;
+    case SP_TUNE_WINO43_IN_NT:
+      sp::g_wino43_in_nt = value >= 0 && value <= 3 ? value : -1;
       return 0;
     default:
       sp::set_error("sp_set_tuning: unknown knob %d", knob);

@@ -203,7 +203,8 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
                 4 * (m_el + m * cout * (1 + (res1 is not None) + (res2 is not None))), (m, cout, "out"))
         return ho, wo
     _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
-            (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision] if ln is None else "f32+ln"))
+            (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision] if ln is None else "f32+ln")
+            + (("rows",) if x.is_bf16 else ()))  # "rows": A staged from bf16 rows (tools/tune_conv.py)
     return ho, wo
 
 
@@ -291,7 +292,7 @@ def force_splitk_config(cfg=None, max_splits=None, min_ktiles=None):
                                0 if min_ktiles is None else int(min_ktiles))
 
 
-TUNE_WINO43_LAYOUT, TUNE_WINO43_IN_ROWS = 1, 2  # include/spotter_hip.h sp_tuning_knob
+TUNE_WINO43_LAYOUT, TUNE_WINO43_IN_NT = 1, 2  # include/spotter_hip.h sp_tuning_knob
 
 
 def set_tuning(knob: int, value: int | None):

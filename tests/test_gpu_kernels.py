@@ -307,9 +307,9 @@ def test_winograd_is_fp32_accurate(dev, case, cfg, wm):
 @pytest.mark.parametrize("shape", [(2, 7, 10, 64, 48), (1, 13, 9, 96, 64), (3, 23, 17, 32, 64)])
 @pytest.mark.parametrize("planes_n", [1, 3])
 def test_winograd_f43_variants_bit_identical(dev, shape, planes_n):
-    """The F(4x4) tuning variants (sp_set_tuning: tile-major workspace, 2/4/8 tile rows per input-transform
-    thread) move memory, not arithmetic: every variant's output equals the default's bit for bit on ragged
-    maps (tile rows not a multiple of the strip), odd and even channel counts, fp32x3 and bf16 planes."""
+    """The F(4x4) tuning variants (sp_set_tuning: tile-major workspace, non-temporal loads / stores in the input
+    transform) move memory, not arithmetic: every variant's output equals the default's bit for bit on ragged
+    maps, odd and even channel counts, fp32x3 and bf16 planes."""
     from spotter_amd import ops
     from spotter_amd.ops import view
 
@@ -335,13 +335,13 @@ def test_winograd_f43_variants_bit_identical(dev, shape, planes_n):
     assert torch.isfinite(ref).all()
     try:
         for layout in (0, 1):
-            for rows in (1, 2, 4, 8):
+            for nt in (0, 1, 2, 3):
                 ops.set_tuning(ops.TUNE_WINO43_LAYOUT, layout)
-                ops.set_tuning(ops.TUNE_WINO43_IN_ROWS, rows)
-                assert torch.equal(run(), ref), (layout, rows)
+                ops.set_tuning(ops.TUNE_WINO43_IN_NT, nt)
+                assert torch.equal(run(), ref), (layout, nt)
     finally:
         ops.set_tuning(ops.TUNE_WINO43_LAYOUT, None)
-        ops.set_tuning(ops.TUNE_WINO43_IN_ROWS, None)
+        ops.set_tuning(ops.TUNE_WINO43_IN_NT, None)
 
 
 @pytest.mark.parametrize("wm", [2, 4])

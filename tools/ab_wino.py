@@ -3,7 +3,7 @@
     python tools/ab_wino.py [--reps 20] [--out ab_wino.json]
 
 For each 3x3 stride-1 shape of the bs32 R101vd forward that takes F(4x4), times the whole Winograd conv
-(input transform + batched split GEMM + output transform) under every (layout, input rows) variant,
+(input transform + batched split GEMM + output transform) under every (layout, non-temporal accesses) variant,
 interleaved over rounds so clock drift hits all variants alike, and checks that every variant's output is
 bit-identical to the default's (the variants reorder memory traffic, not arithmetic). Per-kernel times come
 from a rocprofv3 kernel trace of the same run.
@@ -24,7 +24,7 @@ from spotter_amd.ops import view
 
 SHAPES = [(32, 80, 80, 128, 128), (32, 40, 40, 256, 256), (32, 80, 80, 384, 384), (32, 40, 40, 384, 384),
           (32, 20, 20, 512, 512), (32, 20, 20, 384, 384)]
-VARIANTS = [(0, 1), (0, 2), (0, 4), (1, 1), (1, 2), (1, 4), (0, 8)]
+VARIANTS = [(0, 0), (0, 1), (0, 2), (0, 3), (1, 0), (1, 3)]  # (layout, input-transform non-temporal bits)
 
 
 def timeit(fn, reps):
@@ -41,7 +41,7 @@ def timeit(fn, reps):
 
 def set_variant(v):
     ops.set_tuning(ops.TUNE_WINO43_LAYOUT, None if v is None else v[0])
-    ops.set_tuning(ops.TUNE_WINO43_IN_ROWS, None if v is None else v[1])
+    ops.set_tuning(ops.TUNE_WINO43_IN_NT, None if v is None else v[1])
 
 
 def main():

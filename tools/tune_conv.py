@@ -51,13 +51,16 @@ def workspace(dev):
     return _WS[dev]
 
 
-def time_one(dev, m, cout, K, k, stride, mode, cfg, reps):
+def time_one(dev, m, cout, K, k, stride, mode, cfg, reps, rows=False):
+    """rows: the bf16 variant's form of the layer (A staged from bf16 rows, bf16 rows out)."""
     n, h, w, cin = geometry(m, cout, K, k, stride)
     pad = k // 2
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(n * h * w * cin, device=dev, generator=g)
     wt = torch.randn(cout * K, device=dev, generator=g) * (1.0 / K ** 0.5)
-    out = torch.empty(m * cout, device=dev)
+    out = torch.empty(m * cout, device=dev, dtype=torch.int16 if rows else torch.float32)
+    if rows:
+        x = x.to(torch.bfloat16).view(torch.int16).contiguous()
     if mode == "x3":
         kw = {"wt_planes": ops.split_bf16x3(wt)}
     elif mode == "bf16":
@@ -106,14 +109,16 @@ def main():
     rows = json.load(open(a.detail))
     res = []
     for r in rows:
-        m, cout, K, k, stride, mode = ast.literal_eval(r["shape"])[:6]
+        key = ast.literal_eval(r["shape"])
+        m, cout, K, k, stride, mode = key[:6]
+        rows = len(key) > 6 and key[6] == "rows"
         per_step = r["ms"] / a.steps
         if mode not in a.modes.split(",") or per_step < a.min_ms:
             continue
         launches = r["launches"] / a.steps
         times = {}
         for cfg in (F32_CFGS if mode == "f32" else x3_cfgs):
-            t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps)
+            t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps, rows)
             if t is not None:
                 times[cfg] = round(t, 4)
         if a.cross and mode in ("f32", "x3"):
@@ -123,7 +128,8 @@ def main():
                 if t is not None:
                     times[other + ":" + cfg] = round(t, 4)
         best = min(times, key=times.get)
-        e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "launches_per_step": launches,
+        e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "rows": rows,
+             "launches_per_step": launches,
              "default_ms": times.get("-"), "best_cfg": best, "best_ms": times[best], "times": times,
              "best_same_mode": min((c for c in times if ":" not in c), key=times.get),
              "saving_ms_per_step": round((times.get("-", times[best]) - times[best]) * launches, 4)}
