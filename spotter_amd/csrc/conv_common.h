@@ -296,6 +296,9 @@ __device__ __forceinline__ void epilogue_rowln(const ConvArgs& p, float* tile, c
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s);
 // The LDS-DMA tile configurations of launch_mfma16 (conv_glds.hip); -2 when cfg is not one of them.
 int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s);
+// Tuning: the split mode's slab-epilogue form for the calling thread (4 = direct stores, else the slab
+// store pass; sp_set_tuning SP_TUNE_GLDS_EPILOGUE).
+void set_glds_epilogue(int v);
 // The tile configuration sp_set_conv_config forced for the calling thread (-1: none).
 int forced_cfg();
 // Split-K combine kernel launch (conv_gemm.hip).

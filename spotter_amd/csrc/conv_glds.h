@@ -412,6 +412,94 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
   }
 }
 
+// Variant 4 (round 4): the slab epilogue's residual band by LDS-DMA, but the outputs stored straight from the
+// accumulators (the MFMA layout: one dword store per accumulator register, two 128-byte row segments per
+// wave-instruction) instead of back through the slab. The slab is then free as soon as a round's combine
+// has read it, so the next round's residual DMA is issued before this round's stores and waited for with a
+// count that leaves those stores in flight (the stores are raw buffer stores: always issued, out-of-range
+// rows / columns dropped by the buffer bound, so the count is exact). Same arithmetic as variant 2:
+// bit-identical. fp32 C with plain rows (ldc), res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
+template <int TM, int TN, int NB, bool L16>
+__device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
+                                                  int nb, int lane) {
+  constexpr int WN = TN * 32;
+  constexpr int C4 = WN / 4;
+  constexpr int NI = NB * 32 * C4 / 64;
+  constexpr int NCOL = L16 ? 2 : 1;
+  constexpr int NST = NB * TN * 16;                 // dword stores per round
+  constexpr int WST = NST < 63 ? NST : 63;          // vmcnt field limit: waiting for ≤ 63 still covers the DMA
+  const sp_conv_desc& d = p.d;
+  const int r = lane & 31, h = lane >> 5;
+  float scv[TN][NCOL], shv[TN][NCOL];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      const int n = nb + j * 32 + (L16 ? 16 * k + (lane & 15) : r);
+      const bool ok = n < d.Cout;
+      scv[j][k] = ok && d.scale ? d.scale[n] : 1.0f;
+      shv[j][k] = ok && d.shift ? d.shift[n] : 0.0f;
+    }
+  const uint32_t rbase = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)region);
+  const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
+  const bool res = d.res1 != nullptr;
+  const int nbytes = (int)(((p.M - 1) * d.ldc + d.Cout) * 4);
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(d.C, 0, nbytes, 0x00020000);
+  auto fetch = [&](int64_t mr) {
+#pragma unroll 1
+    for (int u = 0; u < NI; ++u) {
+      const int idx = u * 64 + lane;
+      const int row = idx / C4;
+      const int n = nb + (idx - row * C4) * 4;
+      const int64_t m = mr + row;
+      const void* src = (m < p.M && n < d.Cout) ? static_cast<const void*>(d.res1 + m * d.ldr1 + n)
+                                                 : static_cast<const void*>(zero);
+      glds16(src, rbase + u * 1024);
+    }
+  };
+  if (res) fetch(mb);
+#pragma unroll
+  for (int i0 = 0; i0 < TM; i0 += NB) {
+    const int64_t mr = mb + i0 * 32;
+    if (res) {
+      if (i0 == 0) wait_vmcnt<0>();
+      else wait_vmcnt<WST>();  // this round's residual landed; the previous round's stores may stay in flight
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          const int k = L16 ? (q >> 2) & 1 : 0;
+          float v = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
+          if (res) v += region[(i * 32 + rr) * WN + j * 32 + cc];
+          acc[i0 + i][j][q] = act_apply(v, d.act);
+        }
+    if (res && i0 + NB < TM) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the combine's slab reads are done
+      __builtin_amdgcn_wave_barrier();
+      fetch(mr + NB * 32);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          const int64_t m = mr + i * 32 + rr;
+          const int n = nb + j * 32 + cc;
+          const int off = (m < p.M && n < d.Cout) ? (int)((m * d.ldc + n) * 4) : 0x7ffffffc;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[i0 + i][j][q]), crs, off, 0, 0);
+        }
+  }
+}
+
 // The same slab epilogue for bf16 rows (variant 3: the bf16 variant, C_bf16 out, res1_bf16 or no residual, no
 // res2): the wave's slab (4 bytes per accumulator) holds the residual band as bf16 in its first half (LDS-DMA,
 // 16-byte pieces of 8 channels) and the rounded outputs in its second half; the store pass writes 8-byte
@@ -518,6 +606,8 @@ __device__ __forceinline__ void glds_epilogue(const ConvArgs& p, uint4* smem, in
     epilogue_tile_rd<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
   else if constexpr (EPV == 3)
     epilogue_tile_rd16<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
+  else if constexpr (EPV == 4)
+    epilogue_tile_rdd<TM, TN, C::NB, M16>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
   else
     epilogue_tile<TM, TN, C::NB, M16, PL == 1>(p, region, acc, m0 + wm * TM * 32, n0 + wn * TN * 32, lane);
 }
@@ -608,10 +698,15 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
     const bool f32ok = base && !d.C_bf16 && !d.res1_bf16 && !d.res2_bf16;
     const bool bf16ok = base && d.C_bf16 && !d.res1 && !d.res2 && !d.res2_bf16 &&
                         (!d.res1_bf16 || ((reinterpret_cast<uintptr_t>(d.res1_bf16) & 15) == 0 && d.ldr1 % 8 == 0));
-    epv = f32ok ? 2 : bf16ok ? 3 : 1;
+    // variant 4 (direct stores) on request (epv 4), where its extra conditions hold; else variant 2
+    const bool f32dd = f32ok && !d.res2 && d.out_rows_per_group <= 0 &&
+                       ((a.M - 1) * d.ldc + d.Cout) * 4 < (int64_t(1) << 31) - 4;
+    epv = (epv == 4 && f32dd) ? 4 : f32ok ? 2 : bf16ok ? 3 : 1;
   }
   if constexpr (fit3) {
-    if (planes == 3 && !a16 && t1 && epv == 2)
+    if (planes == 3 && !a16 && t1 && epv == 4)
+      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 4>), grid, blk, 0, s, ab);
+    else if (planes == 3 && !a16 && t1 && epv == 2)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 2>), grid, blk, 0, s, ab);
     else if (planes == 3 && !a16 && t1)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC>), grid, blk, 0, s, ab);

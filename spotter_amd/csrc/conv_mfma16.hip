@@ -1355,6 +1355,9 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
 // 3 = 64×128, 4 = 64×64, 5 = 128×256 (2×4 waves), 6 = 128×64;
 // cfg (LDS-DMA kernel, no A2): 11 = 128×128 3 stages, 12 = 256×128 2 stages, 13 = 64×128 3 stages,
 // 14 = 64×64 3 stages, 15 = 128×256 2 stages, 16 = 128×64 3 stages; < 0 = by shape.
+thread_local int g_glds_epv = -1;
+void set_glds_epilogue(int v) { g_glds_epv = v; }
+
 int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   if (a.A16) {  // bf16 A planes: the LDS-DMA tiles only (the forced / table tile, else the by-shape rule's)
     // bf16 output rows (the bf16 variant's maps): the slab epilogue ("+ 100" → variant 3: res1 by LDS-DMA,
@@ -1430,8 +1433,9 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   if (planes == 3 && !a.A16 && (a.d.res1 || a.d.scale || a.d.shift) && !a.d.row_scale && a.vec_epi &&
       a.splits == 1 && !a.d.C_bf16 &&
       (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
-    cfg += 100;
-  const int gc = cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;  // cfg + 100: the LDS-DMA residual epilogue variant
+    cfg += g_glds_epv == 4 ? 200 : 100;
+  // cfg + 100: the LDS-DMA residual epilogue variant; cfg + 200: its direct-store form
+  const int gc = cfg >= 211 && cfg <= 265 ? cfg - 200 : cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;
   if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;

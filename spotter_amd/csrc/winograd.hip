@@ -529,6 +529,9 @@ extern "C" int sp_set_tuning(int knob, int value) {
     case SP_TUNE_WINO43_IN_NT:
       sp::g_wino43_in_nt = value >= 0 && value <= 3 ? value : -1;
       return 0;
+    case SP_TUNE_GLDS_EPILOGUE:
+      sp::set_glds_epilogue(value == 4 ? 4 : -1);
+      return 0;
     default:
       sp::set_error("sp_set_tuning: unknown knob %d", knob);
       return -1;

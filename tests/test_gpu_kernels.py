@@ -386,6 +386,56 @@ def test_winograd_epilogue_views_and_bf16(dev, wm):
     assert np.abs(d16).max() <= 0.05 * np.abs(plain.cpu().numpy()).max(), np.abs(d16).max()
 
 
+@pytest.mark.parametrize("cfg", ["12", "14", "41", "45", "46", "47", "63", "64"])
+def test_direct_store_epilogue_bit_identical(dev, cfg):
+    """The split mode's slab epilogue with the outputs stored straight from the accumulators (variant 4,
+    sp_set_tuning SP_TUNE_GLDS_EPILOGUE) equals the slab store pass bit for bit: 1×1 convs with BN +
+    residual + relu (the bottleneck expand), BN only, an output slice (ldc > Cout), ragged M and Cout, and
+    the Winograd component GEMM (batched). Untouched output columns stay untouched."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(int(cfg))
+    for rows, K, N, res, ldc in ((1000, 256, 192, True, 192), (777, 128, 96, True, 112), (513, 64, 256, False, 256)):
+        x = T(rng.standard_normal(rows * K).astype(np.float32), dev)
+        wt = T((rng.standard_normal((N, K)) / np.sqrt(K)).astype(np.float32), dev)
+        kw = dict(scale=T(rng.uniform(0.5, 1.5, N).astype(np.float32), dev),
+                  shift=T(rng.standard_normal(N).astype(np.float32), dev), act="relu",
+                  wt_planes=ops.split_bf16x3(wt))
+        if res:
+            kw["res1"] = V(T(rng.standard_normal(rows * N).astype(np.float32), dev), 0, N)
+        outs = []
+        for mode in (None, 4):
+            ops.set_tuning(ops.TUNE_GLDS_EPILOGUE, mode)
+            ops.force_conv_config(cfg)
+            try:
+                o = torch.full((rows * ldc,), 7.0, device=dev)
+                ops.conv2d(V(x, 0, K), 1, 1, rows, K, wt, N, 1, 1, 0, V(o, 0, ldc), **kw)
+                outs.append(o)
+            finally:
+                ops.force_conv_config(None)
+                ops.set_tuning(ops.TUNE_GLDS_EPILOGUE, None)
+        assert torch.equal(outs[0], outs[1]), (cfg, rows, K, N)
+        assert bool((outs[1].view(rows, ldc)[:, N:] == 7.0).all())
+    # the Winograd component GEMM (batched members, BN + residual in the output transform, not here)
+    n, h, w, cin, cout = 2, 9, 11, 64, 96
+    xw = T(rng.standard_normal(n * h * w * cin).astype(np.float32), dev)
+    g = (rng.standard_normal((cout, 3, 3, cin)) / 24).astype(np.float32)
+    pl = T(ops.split_bf16x3_host(ops.winograd_weights_host(g, 4)), dev)
+    work = torch.empty(36 * n * 3 * 3 * (cin + cout) + 64, device=dev)
+    outs = []
+    for mode in (None, 4):
+        ops.set_tuning(ops.TUNE_GLDS_EPILOGUE, mode)
+        try:
+            o = torch.full((n * h * w * cout,), float("nan"), device=dev)
+            ops.conv2d(V(xw, 0, cin), n, h, w, cin, T(g.reshape(cout, -1), dev), cout, 3, 1, 1, V(o, 0, cout),
+                       wino=(pl, work, 4))
+            outs.append(o)
+        finally:
+            ops.set_tuning(ops.TUNE_GLDS_EPILOGUE, None)
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv2d_bf16_a_rows_bit_identical(dev):
     """sp_conv2d with A given as bf16 rows (sp_conv_desc.A_bf16, the bf16 variant's maps) equals the launch on
     the same values as fp32 A (rounded to bf16 per fragment inside the GEMM, exactly): 1×1 and 3×3 stride-2

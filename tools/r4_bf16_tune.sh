@@ -14,3 +14,9 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 
 timeout -k 10 300 python -u tools/ab_wino.py --out $O/ab_wino.json > $O/ab_wino.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_wino -o run -- python3 $GRAFT_REPO_ROOT/tools/ab_wino.py --rounds 1 --reps 5 --out /tmp/x.json > $GRAFT_REPO_ROOT/$O/prof_wino.log 2>&1
+cd $GRAFT_REPO_ROOT
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "direct_store" > $O/t_dstore.log 2>&1
+timeout -k 10 400 python -u tools/ab_glds.py --pairs 146:246,147:247,145:245,163:263,112:212,141:241 --shapes 0,9,10,11,1,4,2 --out $O/ab_dstore.jsonl > $O/ab_dstore.log 2>&1
+for c in 46 47 63; do SPOTTER_HIP_LIB=spotter_amd/_diag/libspotter_stamp.so timeout -k 10 120 python -u tools/microbench/glds_stamps.py 0 --cfg $c >> $O/stamps.jsonl 2>>$O/stamps.err; done
+SPOTTER_HIP_LIB=spotter_amd/_diag/libspotter_stamp.so timeout -k 10 120 python -u tools/microbench/glds_stamps.py 1 --cfg 33 >> $O/stamps.jsonl 2>>$O/stamps.err
