@@ -155,8 +155,6 @@ int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles);
 /* Tuning knobs of this thread's later launches (ABI v11; value -1 = the product default), for same-process
  * A/B measurements; nothing on the product path calls it. */
 enum sp_tuning_knob {
-  SP_TUNE_WINO43_LAYOUT = 1,  /* F(4x4) workspace: 0 component-major [36][T][C], 1 tile-major [T][36][C] */
-  SP_TUNE_WINO43_IN_NT = 2,   /* F(4x4) input transform: bit 0 non-temporal map loads, bit 1 non-temporal V stores */
   SP_TUNE_GLDS_EPILOGUE = 3,  /* split-mode slab epilogue: 4 = outputs stored from the accumulators, else the slab pass */
 };
 int sp_set_tuning(int knob, int value);

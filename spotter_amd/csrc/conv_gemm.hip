@@ -440,3 +440,14 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
   if (a.K <= 128 || d->Cout <= 64 || tiles64 < 3000) return launch<1, 1, 0>(a, s);
   return launch<1, 2, 0>(a, s);
 }
+
+extern "C" int sp_set_tuning(int knob, int value) {
+  switch (knob) {
+    case SP_TUNE_GLDS_EPILOGUE:
+      sp::set_glds_epilogue(value == 4 ? 4 : -1);
+      return 0;
+    default:
+      sp::set_error("sp_set_tuning: unknown knob %d", knob);
+      return -1;
+  }
+}

@@ -414,11 +414,12 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
 
 // Variant 4 (round 4): the slab epilogue's residual band by LDS-DMA, but the outputs stored straight from the
 // accumulators (the MFMA layout: one dword store per accumulator register, two 128-byte row segments per
-// wave-instruction) instead of back through the slab. The slab is then free as soon as a round's combine
-// has read it, so the next round's residual DMA is issued before this round's stores and waited for with a
-// count that leaves those stores in flight (the stores are raw buffer stores: always issued, out-of-range
-// rows / columns dropped by the buffer bound, so the count is exact). Same arithmetic as variant 2:
-// bit-identical. fp32 C with plain rows (ldc), res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
+// wave-instruction; raw buffer stores, out-of-range rows / columns dropped by the buffer bound) instead of
+// back through the slab. The slab is then free as soon as a round's combine has read it, so the next
+// round's residual DMA is issued before this round's stores. Its wait stays a full vmcnt(0): a counted wait
+// that left the stores in flight measured wrong data on gfx950 (stores and loads do not retire in issue
+// order against each other). Same arithmetic as variant 2: bit-identical. fp32 C with plain rows (ldc),
+// res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
 template <int TM, int TN, int NB, bool L16>
 __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
                                                   int nb, int lane) {
@@ -426,8 +427,6 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
   constexpr int C4 = WN / 4;
   constexpr int NI = NB * 32 * C4 / 64;
   constexpr int NCOL = L16 ? 2 : 1;
-  constexpr int NST = NB * TN * 16;                 // dword stores per round
-  constexpr int WST = NST < 63 ? NST : 63;          // vmcnt field limit: waiting for ≤ 63 still covers the DMA
   const sp_conv_desc& d = p.d;
   const int r = lane & 31, h = lane >> 5;
   float scv[TN][NCOL], shv[TN][NCOL];
@@ -462,10 +461,7 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
 #pragma unroll
   for (int i0 = 0; i0 < TM; i0 += NB) {
     const int64_t mr = mb + i0 * 32;
-    if (res) {
-      if (i0 == 0) wait_vmcnt<0>();
-      else wait_vmcnt<WST>();  // this round's residual landed; the previous round's stores may stay in flight
-    }
+    if (res) wait_vmcnt<0>();
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll

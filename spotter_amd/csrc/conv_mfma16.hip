@@ -1371,6 +1371,8 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     int c = -1;
     const auto tiles = [&](int bm, int bn) { return ((a.M + bm - 1) / bm) * ((a.d.Cout + bn - 1) / bn); };
     if (a.d.Cout <= 64) c = tiles(128, 64) >= 192 ? 16 : 14;
+    // 3×3s on bf16 rows: 256×128 on 16x16x32 MFMAs beat 256×256 by 1.2-1.3× (profiles/r4/bf16/)
+    else if (a.d.KH == 3 && a.d.Cout % 128 == 0 && tiles(256, 128) >= 192) c = 41;
     else if (a.d.Cout % 256 == 0 && a.K >= 512 && tiles(256, 256) >= 192) c = 33;
     else if (a.d.Cout % 128 == 0 && tiles(128, 128) >= 192) c = planes == 3 ? 46 : 45;
     else if (tiles(256, 128) >= 192) c = 12;

@@ -157,11 +157,11 @@ struct VT {
 
 // VW consecutive channels per thread (1 or 2: the launch takes 1 on maps too small to fill the chip
 // with 2-channel threads).
-// V element (component k, tile t, channel c) lives at V[k·cstride + t·tstride + c]: component-major
-// (cstride = T·Cin, tstride = Cin, the default) or tile-major (cstride = Cin, tstride = 36·Cin: the 36
-// components of a tile side by side, so both transforms touch one compact region per tile).
-// NT: bit 0 non-temporal loads of the map, bit 1 non-temporal stores of V (tuning variants, sp_set_tuning).
-template <int VW, int NT = 0>
+// V element (component k, tile t, channel c) lives at V[k·cstride + t·tstride + c]: component-major,
+// cstride = T·Cin, tstride = Cin. (Round 4 measured the tile-major layout — the 36 components of a tile
+// side by side — non-temporal map loads / V stores, and 2-8 tile rows per thread sharing the patch
+// overlap: within ±1 % or slower on the C2 shapes, profiles/r4/wino/.)
+template <int VW>
 __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restrict__ x, int64_t lda, int h, int w,
                                                           int cvn, int th, int tw, int64_t T,
                                                           float* __restrict__ V, int64_t tstride, int64_t cstride) {
@@ -184,9 +184,8 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int xx = x0 + j;
-        const vf* src = reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c);
         dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
-                    ? ((NT & 1) ? __builtin_nontemporal_load(src) : *src)
+                    ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
                     : vf(0.f);
       }
 #pragma unroll
@@ -207,10 +206,7 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
 #pragma unroll
         for (int i = 0; i < 6; ++i)
           if (kBT43[a][i] != 0.f) v = __builtin_elementwise_fma(vf(kBT43[a][i]), q[i][bb], v);
-        if constexpr ((NT & 2) != 0)
-          __builtin_nontemporal_store(v, reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane));
-        else
-          *reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane) = v;
+        *reinterpret_cast<vf*>(dst + (a * 6 + bb) * plane) = v;
       }
   }
 }
@@ -300,13 +296,6 @@ int wino43_out_vw() {
   return f ? f : 1;
 }
 
-// Tuning knobs of the F(4×4) path (sp_set_tuning, per calling thread; -1 = the product default): the
-// workspace layout (0 component-major, 1 tile-major) and the input transform's non-temporal accesses.
-thread_local int g_wino43_layout = -1;
-thread_local int g_wino43_in_nt = -1;
-int wino43_layout() { return g_wino43_layout >= 0 ? g_wino43_layout : 0; }
-int wino43_in_nt() { return g_wino43_in_nt >= 0 ? g_wino43_in_nt : 0; }
-
 int stream_grid(int64_t work) {
   int64_t g = (work + 255) / 256;
   const int64_t cap = (int64_t)g_num_cus * 16;
@@ -374,21 +363,13 @@ int wino_input(const char* what, const sp_conv_desc* d, float* work, int64_t wor
     hipLaunchKernelGGL(wino_in_f23_x2_kernel, dim3(stream_grid(pairs * cin4)), dim3(256), 0, as_stream(stream),
                        d->A, d->lda, d->H, d->W, cin4, th, tw, (int64_t)d->N, work, (int64_t)d->Cin);
   } else {
-    const bool tm = wino43_layout() == 1;
-    const int64_t ts = tm ? (int64_t)NC * d->Cin : d->Cin, cs = tm ? (int64_t)d->Cin : T * d->Cin;
-    const int vw = wino43_in_vw(T * d->Cin), nt = wino43_in_nt();
-    const dim3 gr(stream_grid(T * d->Cin / vw));
-#define SP_WINO_IN(VW, NT)                                                                                         \
-  hipLaunchKernelGGL((wino_in_f43_kernel<VW, NT>), gr, dim3(256), 0, as_stream(stream), d->A, d->lda, d->H, d->W,  \
-                     d->Cin / VW, th, tw, T, work, ts, cs)
-    if (vw == 1) {
-      if (nt == 1) SP_WINO_IN(1, 1); else if (nt == 2) SP_WINO_IN(1, 2); else if (nt == 3) SP_WINO_IN(1, 3);
-      else SP_WINO_IN(1, 0);
-    } else {
-      if (nt == 1) SP_WINO_IN(2, 1); else if (nt == 2) SP_WINO_IN(2, 2); else if (nt == 3) SP_WINO_IN(2, 3);
-      else SP_WINO_IN(2, 0);
-    }
-#undef SP_WINO_IN
+    const int64_t ts = d->Cin, cs = T * d->Cin;
+    if (wino43_in_vw(T * d->Cin) == 1)
+      hipLaunchKernelGGL(wino_in_f43_kernel<1>, dim3(stream_grid(T * d->Cin)), dim3(256), 0, as_stream(stream),
+                         d->A, d->lda, d->H, d->W, d->Cin, th, tw, T, work, ts, cs);
+    else
+      hipLaunchKernelGGL(wino_in_f43_kernel<2>, dim3(stream_grid(T * d->Cin / 2)), dim3(256), 0, as_stream(stream),
+                         d->A, d->lda, d->H, d->W, d->Cin / 2, th, tw, T, work, ts, cs);
   }
   return check_launch(what);
 }
@@ -434,12 +415,6 @@ int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, 
   g.bs_a = T * d->Cin;
   g.bs_w = (int64_t)d->Cout * d->Cin;
   g.bs_c = T * d->Cout;
-  if (MT == 4 && wino43_layout() == 1) {  // tile-major V / M: component k of tile t at t·NC·C + k·C
-    g.d.lda = (int64_t)NC * d->Cin;
-    g.d.ldc = (int64_t)NC * d->Cout;
-    g.bs_a = d->Cin;
-    g.bs_c = d->Cout;
-  }
   // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py,
   // profiles/r2/tune_wino_x3.json: bs32 shapes, NC × T rows): 256×128 k16 (cfg 44) for the tallest
   // batches and for the wide ones from 400000 rows (bs32 80²×384: 1.25 vs 1.32 ms on two boxes,
@@ -473,8 +448,7 @@ int wino_output(const char* what, const sp_conv_desc* d, const float* work, int6
     hipLaunchKernelGGL(wino_out_f23_kernel, dim3(stream_grid(T * cout4)), dim3(256), 0, as_stream(stream),
                        work + wino_v_floats(NC, T, d->Cin), T, cout4, th, tw, *d);
   } else {
-    const bool tm = wino43_layout() == 1;
-    const int64_t ts = tm ? (int64_t)NC * d->Cout : d->Cout, cs = tm ? (int64_t)d->Cout : T * d->Cout;
+    const int64_t ts = d->Cout, cs = T * d->Cout;
     if (wino43_out_vw() == 1)
       hipLaunchKernelGGL(wino_out_f43_kernel<1>, dim3(stream_grid(T * d->Cout)), dim3(256), 0, as_stream(stream),
                          work + wino_v_floats(NC, T, d->Cin), T, d->Cout, th, tw, *d, ts, cs);
@@ -519,21 +493,4 @@ extern "C" int sp_winograd_f43_gemm(const sp_conv_desc* d, const uint16_t* wt_wi
 
 extern "C" int sp_winograd_f43_output(const sp_conv_desc* d, const float* work, int64_t work_elems, void* stream) {
   return sp::wino_output<4>("sp_winograd_f43_output", d, work, work_elems, stream);
-}
-
-extern "C" int sp_set_tuning(int knob, int value) {
-  switch (knob) {
-    case SP_TUNE_WINO43_LAYOUT:
-      sp::g_wino43_layout = value == 0 || value == 1 ? value : -1;
-      return 0;
-    case SP_TUNE_WINO43_IN_NT:
-      sp::g_wino43_in_nt = value >= 0 && value <= 3 ? value : -1;
-      return 0;
-    case SP_TUNE_GLDS_EPILOGUE:
-      sp::set_glds_epilogue(value == 4 ? 4 : -1);
-      return 0;
-    default:
-      sp::set_error("sp_set_tuning: unknown knob %d", knob);
-      return -1;
-  }
 }

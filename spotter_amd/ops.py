@@ -292,7 +292,7 @@ def force_splitk_config(cfg=None, max_splits=None, min_ktiles=None):
                                0 if min_ktiles is None else int(min_ktiles))
 
 
-TUNE_WINO43_LAYOUT, TUNE_WINO43_IN_NT, TUNE_GLDS_EPILOGUE = 1, 2, 3  # include/spotter_hip.h sp_tuning_knob
+TUNE_GLDS_EPILOGUE = 3  # include/spotter_hip.h sp_tuning_knob
 
 
 def set_tuning(knob: int, value: int | None):

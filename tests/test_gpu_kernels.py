@@ -304,46 +304,6 @@ def test_winograd_is_fp32_accurate(dev, case, cfg, wm):
     assert ew <= 1e-5 * scale, (ew, scale)
 
 
-@pytest.mark.parametrize("shape", [(2, 7, 10, 64, 48), (1, 13, 9, 96, 64), (3, 23, 17, 32, 64)])
-@pytest.mark.parametrize("planes_n", [1, 3])
-def test_winograd_f43_variants_bit_identical(dev, shape, planes_n):
-    """The F(4x4) tuning variants (sp_set_tuning: tile-major workspace, non-temporal loads / stores in the input
-    transform) move memory, not arithmetic: every variant's output equals the default's bit for bit on ragged
-    maps, odd and even channel counts, fp32x3 and bf16 planes."""
-    from spotter_amd import ops
-    from spotter_amd.ops import view
-
-    n, h, w, cin, cout = shape
-    rng = np.random.default_rng(seed(shape, planes_n))
-    x = T(rng.standard_normal(n * h * w * cin).astype(np.float32), dev)
-    wt = (rng.standard_normal((cout, 3, 3, cin)) / np.sqrt(9 * cin)).astype(np.float32)
-    u = ops.winograd_weights_host(wt, 4)
-    pl = T(ops.split_bf16x3_host(u), dev) if planes_n == 3 else T(
-        ops.bf16_bits(u).reshape(1, -1).view(np.int16), dev)
-    tiles = n * ((h + 3) // 4) * ((w + 3) // 4)
-    work = torch.empty(36 * tiles * (cin + cout) + 64, device=dev)
-    wk = T(wt.reshape(cout, -1), dev)
-    sh = T(rng.standard_normal(cout).astype(np.float32), dev)
-
-    def run():
-        out = torch.full((n * h * w * cout,), float("nan"), device=dev)
-        ops.conv2d(view(x, cin), n, h, w, cin, wk, cout, 3, 1, 1, view(out, cout), shift=sh, act="silu",
-                   wino=(pl, work, 4))
-        return out
-
-    ref = run()
-    assert torch.isfinite(ref).all()
-    try:
-        for layout in (0, 1):
-            for nt in (0, 1, 2, 3):
-                ops.set_tuning(ops.TUNE_WINO43_LAYOUT, layout)
-                ops.set_tuning(ops.TUNE_WINO43_IN_NT, nt)
-                assert torch.equal(run(), ref), (layout, nt)
-    finally:
-        ops.set_tuning(ops.TUNE_WINO43_LAYOUT, None)
-        ops.set_tuning(ops.TUNE_WINO43_IN_NT, None)
-
-
 @pytest.mark.parametrize("wm", [2, 4])
 def test_winograd_epilogue_views_and_bf16(dev, wm):
     """The Winograd path's epilogue matches the direct conv's: BN scale / shift, res1 (pre-act), act,
