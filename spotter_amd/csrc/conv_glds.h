@@ -418,8 +418,9 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
 // back through the slab. The slab is then free as soon as a round's combine has read it, so the next
 // round's residual DMA is issued before this round's stores. Its wait stays a full vmcnt(0): a counted wait
 // that left the stores in flight measured wrong data on gfx950 (stores and loads do not retire in issue
-// order against each other). Same arithmetic as variant 2: bit-identical. fp32 C with plain rows (ldc),
-// res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
+// order against each other). The results go to a local array, not back into the accumulators (writing them
+// in place made hipcc store one register sixteen times). Same arithmetic as variant 2: bit-identical. fp32 C
+// with plain rows (ldc), res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
 template <int TM, int TN, int NB, bool L16>
 __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
                                                   int nb, int lane) {
@@ -460,6 +461,7 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
   if (res) fetch(mb);
 #pragma unroll
   for (int i0 = 0; i0 < TM; i0 += NB) {
+    float o[NB][TN][16];
     const int64_t mr = mb + i0 * 32;
     if (res) wait_vmcnt<0>();
 #pragma unroll
@@ -473,7 +475,7 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
           const int k = L16 ? (q >> 2) & 1 : 0;
           float v = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
           if (res) v += region[(i * 32 + rr) * WN + j * 32 + cc];
-          acc[i0 + i][j][q] = act_apply(v, d.act);
+          o[i][j][q] = act_apply(v, d.act);
         }
     if (res && i0 + NB < TM) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the combine's slab reads are done
@@ -491,7 +493,7 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
           const int64_t m = mr + i * 32 + rr;
           const int n = nb + j * 32 + cc;
           const int off = (m < p.M && n < d.Cout) ? (int)((m * d.ldc + n) * 4) : 0x7ffffffc;
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[i0 + i][j][q]), crs, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o[i][j][q]), crs, off, 0, 0);
         }
   }
 }
