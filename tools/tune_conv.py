@@ -129,7 +129,6 @@ def main():
                     times[other + ":" + cfg] = round(t, 4)
         best = min(times, key=times.get)
         e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "rows": rows,
-             "wino": len(key) > 6 and key[6] == "wino",
              "launches_per_step": launches,
              "default_ms": times.get("-"), "best_cfg": best, "best_ms": times[best], "times": times,
              "best_same_mode": min((c for c in times if ":" not in c), key=times.get),
