@@ -415,19 +415,20 @@ int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, 
   g.bs_a = T * d->Cin;
   g.bs_w = (int64_t)d->Cout * d->Cin;
   g.bs_c = T * d->Cout;
-  // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py,
-  // profiles/r2/tune_wino_x3.json: bs32 shapes, NC × T rows): 256×128 k16 (cfg 44) for the tallest
-  // batches and for the wide ones from 400000 rows (bs32 80²×384: 1.25 vs 1.32 ms on two boxes,
-  // profiles/r2/wino43_in_remap_ab.json, wino43_vw_ab.json), 128×128 k16 at two workgroups per CU (cfg 46) otherwise, its 16x16x32 form (cfg 47) for
-  // Cout >= 512, 64×64 (cfg 14) when Cout is not a multiple of 128 or the batch is short (fewer than
-  // 12000 NC × T rows: the bs1 / bs8 maps, where the larger tiles leave CUs idle; 1.4x at bs1 40²×384,
-  // profiles/r2/tune_wino_f43_bs1.json, profiles/r2/tune_wino_x3_bs8_bs1.json)
+  // tile: a forced LDS-DMA configuration (tuning), else the measured choice (tools/tune_wino.py): 64×64 (cfg
+  // 14) when Cout is not a multiple of 128 or the batch is short (fewer than 12000 NC × T rows: the bs1 / bs8
+  // maps, where the larger tiles leave CUs idle; 1.4x at bs1 40²×384, profiles/r2/tune_wino_f43_bs1.json,
+  // tune_wino_x3_bs8_bs1.json); else the direct-store epilogue forms (cfg + 200, round 4,
+  // profiles/r4/x3/tune_wino_f43_r4.json, whole-conv times at bs32 vs the round-3 choice): 128×128 k32 on
+  // 16x16x32 MFMAs (247) for the wide batches from 400000 rows (80²×384: 1.162 vs 1.241 ms for cfg 44),
+  // 128×128 k16 at four workgroups per CU (246) for Cout <= 256 (40²×256: 0.177 vs 0.184; 80²×128: 0.268 vs
+  // 0.282), 128×128 k32 (245) otherwise (40²×384: 0.308 vs 0.327; 20²×512: 0.140 vs 0.150 for cfg 47).
   int cfg = forced_cfg();
   if (cfg < 0) {
     if (d->Cout % 128 || T * NC < 12000) cfg = 14;
-    else if (d->Cout >= 512) cfg = 47;
-    else if (T * NC >= 640000 || (T * NC >= 400000 && d->Cout >= 384)) cfg = 44;
-    else cfg = 46;
+    else if (T * NC >= 400000 && d->Cout >= 384) cfg = 247;
+    else if (d->Cout <= 256) cfg = 246;
+    else cfg = 245;
   }
   const int rc = launch_glds_cfg(g, planes, cfg, as_stream(stream));
   if (rc == -2) {

@@ -204,7 +204,8 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         return ho, wo
     _launch("conv", "sp_conv2d", (C.byref(d), stream()), 2 * m * cout * k * k * cin, nbytes,
             (m, cout, k * k * cin, k, stride, ("f32", "bf16", "x3")[d.precision] if ln is None else "f32+ln")
-            + (("rows",) if x.is_bf16 else ()))  # "rows": A staged from bf16 rows (tools/tune_conv.py)
+            + (("rows",) if x.is_bf16 else ())  # "rows": A staged from bf16 rows (tools/tune_conv.py)
+            + ("epi:" + ("res" if res1 is not None else "bn" if scale is not None or shift is not None else "none"),))
     return ho, wo
 
 

@@ -262,7 +262,7 @@ WINO_CASES = [
     (1, 1, 1, 32, 64, "gelu"),       # one pixel: a single, mostly padded tile
     (2, 40, 40, 256, 256, None),     # the backbone stage-3 conv2 shape at bs2
 ]
-WINO_CFGS = [None, "63", "33", "14", "45", "44"]
+WINO_CFGS = [None, "63", "33", "14", "45", "44", "246", "247"]  # + 200: the direct-store epilogue forms
 
 
 @pytest.mark.parametrize("case", WINO_CASES)

@@ -26,7 +26,17 @@ def main():
     ap.add_argument("tunes", nargs="+")
     ap.add_argument("--tag", required=True)
     ap.add_argument("--min-gain", type=float, default=0.02)
+    ap.add_argument("--detail", action="append", default=[],
+                    help="bench.py --detail file: its Winograd component GEMMs (batched, tiled by wino_gemm's own "
+                         "rule, not the table) are skipped")
     a = ap.parse_args()
+    import ast
+    wino = set()
+    for p in a.detail:
+        for r in json.load(open(p)):
+            k = ast.literal_eval(r["shape"])
+            if len(k) > 6 and k[6] == "wino":
+                wino.add(tuple(k[:3]))
     lines = open(TABLE).read().split("\n")
     ent, order = {}, []
     first = last = None
@@ -42,6 +52,8 @@ def main():
         for e in json.load(open(p))["shapes"]:
             planes = {"x3": 3, "bf16": 1}.get(e["mode"], 0)
             key = (e["m"], e["cout"], e["K"], e["k"], e["stride"], planes)
+            if (e["m"], e["cout"], e["K"]) in wino:
+                continue
             times = {c: t for c, t in e["times"].items() if ":" not in c}
             if not e.get("rows", False):  # fp32-A launches: the bf16-row-only tiles are not theirs
                 times = {c: t for c, t in times.items() if c == "-" or not 52 <= int(c) <= 56}

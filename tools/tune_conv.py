@@ -51,8 +51,10 @@ def workspace(dev):
     return _WS[dev]
 
 
-def time_one(dev, m, cout, K, k, stride, mode, cfg, reps, rows=False):
-    """rows: the bf16 variant's form of the layer (A staged from bf16 rows, bf16 rows out)."""
+def time_one(dev, m, cout, K, k, stride, mode, cfg, reps, rows=False, epi="none"):
+    """rows: the bf16 variant's form of the layer (A staged from bf16 rows, bf16 rows out); epi: the launch's
+    epilogue as the engine runs it ("res": BN + residual + relu, "bn": BN + relu, "none"), which decides
+    between the plain and the slab / direct-store epilogue forms."""
     n, h, w, cin = geometry(m, cout, K, k, stride)
     pad = k // 2
     g = torch.Generator(device=dev).manual_seed(0)
@@ -68,6 +70,14 @@ def time_one(dev, m, cout, K, k, stride, mode, cfg, reps, rows=False):
     else:
         kw = {}
     ops.force_conv_config(None if cfg == "-" else cfg)
+
+    if epi in ("res", "bn"):
+        kw["scale"] = torch.rand(cout, device=dev, generator=g) + 0.5
+        kw["shift"] = torch.randn(cout, device=dev, generator=g)
+        kw["act"] = "relu"
+    if epi == "res":
+        r = torch.randn(m * cout, device=dev, generator=g)
+        kw["res1"] = view(r.to(torch.bfloat16).view(torch.int16).contiguous() if rows else r, cout)
 
     def run():
         ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, stride, pad, view(out, cout), workspace=workspace(dev),
@@ -111,14 +121,15 @@ def main():
     for r in rows:
         key = ast.literal_eval(r["shape"])
         m, cout, K, k, stride, mode = key[:6]
-        rows = len(key) > 6 and key[6] == "rows"
+        rows = "rows" in key[6:]
+        epi = next((t[4:] for t in key[6:] if isinstance(t, str) and t.startswith("epi:")), "none")
         per_step = r["ms"] / a.steps
         if mode not in a.modes.split(",") or per_step < a.min_ms:
             continue
         launches = r["launches"] / a.steps
         times = {}
         for cfg in (F32_CFGS if mode == "f32" else x3_cfgs):
-            t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps, rows)
+            t = time_one(dev, m, cout, K, k, stride, mode, cfg, a.reps, rows, epi)
             if t is not None:
                 times[cfg] = round(t, 4)
         if a.cross and mode in ("f32", "x3"):
@@ -128,7 +139,8 @@ def main():
                 if t is not None:
                     times[other + ":" + cfg] = round(t, 4)
         best = min(times, key=times.get)
-        e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "rows": rows,
+        e = {"m": m, "cout": cout, "K": K, "k": k, "stride": stride, "mode": mode, "rows": rows, "epi": epi,
+             "wino": len(key) > 6 and key[6] == "wino",
              "launches_per_step": launches,
              "default_ms": times.get("-"), "best_cfg": best, "best_ms": times[best], "times": times,
              "best_same_mode": min((c for c in times if ":" not in c), key=times.get),
