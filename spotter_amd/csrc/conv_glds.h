@@ -416,10 +416,11 @@ __device__ __forceinline__ void epilogue_tile_rd(const ConvArgs& p, float* regio
 // accumulators (the MFMA layout: one dword store per accumulator register, two 128-byte row segments per
 // wave-instruction; raw buffer stores, out-of-range rows / columns dropped by the buffer bound) instead of
 // back through the slab. The slab is then free as soon as a round's combine has read it, so the next
-// round's residual DMA is issued before this round's stores. Its wait stays a full vmcnt(0): a counted wait
-// that left the stores in flight measured wrong data on gfx950 (stores and loads do not retire in issue
-// order against each other). The results go to a local array, not back into the accumulators (writing them
-// in place made hipcc store one register sixteen times). Same arithmetic as variant 2: bit-identical. fp32 C
+// round's residual DMA is issued before this round's stores. Its wait stays a full vmcnt(0): the stores share
+// the counter with the DMA, and the compiler's own waitcnt model treats mixed loads and stores on one vmcnt as
+// unordered, so a count that left the stores in flight would not prove the DMA landed. The results go to a
+// local array, not back into the accumulators (writing them in place made hipcc store one register sixteen
+// times: every row but the first wrong, tests/test_gpu_kernels.py::test_direct_store_epilogue_bit_identical). Same arithmetic as variant 2: bit-identical. fp32 C
 // with plain rows (ldc), res1 fp32 or none, no res2 / row_scale; C span < 2^31 bytes.
 template <int TM, int TN, int NB, bool L16>
 __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
