@@ -71,17 +71,9 @@ struct GldsCfg {
 // instead of a zero block. Both split A pair-wise (split_frag_pk). Bit-identical outputs, measured
 // 1.02-1.09× over the previous form (element-wise split, general addressing everywhere) on the C2
 // shapes (profiles/r3/ab_glds_v2.jsonl, tools/ab_glds.py).
-struct NoPrefetch {
-  __device__ void operator()() const {}
-};
-
-// pre: called once, in the k-step before the last one (after that step's DMA issue), to start the
-// epilogue's own loads early (variant 5); NoPrefetch for every other kernel.
-template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int APL = 0,
-          typename Pre = NoPrefetch>
+template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, bool M16, int V = 1, int APL = 0>
 __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg, int bi, int kt0, int kt1,
-                                          f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1],
-                                          Pre pre = Pre()) {
+                                          f32x16 (&acc)[TM][TN], f32x4 (&acc4)[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1]) {
   using C = GldsCfg<WM, WN, TM, TN, PL, NS, BK, APL>;
   static_assert(!M16 || BK == 32, "16x16x32 steps need a 32-deep stage");
   constexpr int NT = C::NT, RA = C::RA, RB = C::RB, CA = C::CA, CB = C::CB, GA = C::GA, GB = C::GB;
@@ -318,7 +310,6 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     if (kt + NS - 1 < nk)
 #endif
       issue(kt0 + kt + NS - 1, (kt + NS - 1) % NS);
-    if (kt == (nk >= 2 ? nk - 2 : 0)) pre();
     compute(kt % NS);
   }
 }
@@ -582,66 +573,6 @@ __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* reg
   }
 }
 
-// Variant 5 (round 4): the residual band prefetched into registers in the MFMA layout during the k-step before
-// the last (glds_main's hook), so the epilogue is the combine and the direct stores only, without LDS and
-// without a wait on HBM. Costs TM·TN·16 VGPRs per lane for the whole tile's residual (the kernel is built
-// without an occupancy floor). fp32 res1 (required), fp32 C with plain rows; bit-identical to variants 2 / 4.
-template <int TM, int TN, bool L16>
-__device__ __forceinline__ void res_prefetch(const ConvArgs& p, float (&rv)[TM][TN][16], int64_t mb, int nb,
-                                             int lane) {
-  const sp_conv_desc& d = p.d;
-  const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
-        const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
-        const int64_t m = mb + i * 32 + rr;
-        const int n = nb + j * 32 + cc;
-        rv[i][j][q] = (m < p.M && n < d.Cout) ? d.res1[m * d.ldr1 + n] : 0.f;
-      }
-}
-
-template <int TM, int TN, bool L16>
-__device__ __forceinline__ void epilogue_regs(const ConvArgs& p, f32x16 (&acc)[TM][TN], const float (&rv)[TM][TN][16],
-                                              int64_t mb, int nb, int lane) {
-  constexpr int NCOL = L16 ? 2 : 1;
-  const sp_conv_desc& d = p.d;
-  const int r = lane & 31, h = lane >> 5;
-  float scv[TN][NCOL], shv[TN][NCOL];
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int k = 0; k < NCOL; ++k) {
-      const int n = nb + j * 32 + (L16 ? 16 * k + (lane & 15) : r);
-      const bool ok = n < d.Cout;
-      scv[j][k] = ok && d.scale ? d.scale[n] : 1.0f;
-      shv[j][k] = ok && d.shift ? d.shift[n] : 0.0f;
-    }
-  const int nbytes = (int)(((p.M - 1) * d.ldc + d.Cout) * 4);
-  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(d.C, 0, nbytes, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
-        const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
-        const int k = L16 ? (q >> 2) & 1 : 0;
-        float v = fmaf(acc[i][j][q], scv[j][k], shv[j][k]);
-        v += rv[i][j][q];
-        const float o = act_apply(v, d.act);
-        const int64_t m = mb + i * 32 + rr;
-        const int n = nb + j * 32 + cc;
-        const int off = (m < p.M && n < d.Cout) ? (int)((m * d.ldc + n) * 4) : 0x7ffffffc;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, o), crs, off, 0, 0);
-      }
-}
-
 // Fused epilogue of tile `wg` through the LDS (the caller has synchronised the stages away).
 // Batched launches: the caller passes the batch member's own output slab in p.d.C and the tile
 // index within that member.
@@ -698,26 +629,6 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void conv_glds_kernel(const Conv
   f32x16 acc[TM][TN];
   f32x4 acc4[M16 ? 2 * TM : 1][M16 ? 2 * TN : 1];
   glds_zero<TM, TN, M16>(acc, acc4);
-  if constexpr (EPV == 5) {  // residual prefetched into registers; the epilogue touches no LDS
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int tilesN = (p.d.Cout + C::BN - 1) / C::BN;
-    const int mt = wg / tilesN;
-    const int64_t mb = (int64_t)mt * C::BM + (wave / WN) * TM * 32;
-    const int nb = (wg - mt * tilesN) * C::BN + (wave % WN) * TN * 32;
-    float rv[TM][TN][16];
-    glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V, APL>(p, smem, wg, bi, kt0, kt1, acc, acc4,
-                                                       [&]() { res_prefetch<TM, TN, M16>(p, rv, mb, nb, lane); });
-    if constexpr (M16) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int q = 0; q < 16; ++q) acc[i][j][q] = acc4[2 * i + (q >> 3)][2 * j + ((q >> 2) & 1)][q & 3];
-    }
-    epilogue_regs<TM, TN, M16>(p, acc, rv, mb, nb, lane);
-    return;
-  }
   glds_main<WM, WN, TM, TN, PL, NS, BK, M16, V, APL>(p, smem, wg, bi, kt0, kt1, acc, acc4);
   GLDS_STAMP(2);
   __syncthreads();  // every wave done reading the stages before the epilogue reuses the LDS
@@ -789,12 +700,10 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
     // variant 4 (direct stores) on request (epv 4), where its extra conditions hold; else variant 2
     const bool f32dd = f32ok && !d.res2 && d.out_rows_per_group <= 0 &&
                        ((a.M - 1) * d.ldc + d.Cout) * 4 < (int64_t(1) << 31) - 4;
-    epv = (epv == 5 && f32dd && d.res1 && a.batch == 1) ? 5 : (epv >= 4 && f32dd) ? 4 : f32ok ? 2 : bf16ok ? 3 : 1;
+    epv = (epv == 4 && f32dd) ? 4 : f32ok ? 2 : bf16ok ? 3 : 1;
   }
   if constexpr (fit3) {
-    if (planes == 3 && !a16 && t1 && epv == 5)
-      hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, 1, 0, 5>), grid, blk, 0, s, ab);
-    else if (planes == 3 && !a16 && t1 && epv == 4)
+    if (planes == 3 && !a16 && t1 && epv == 4)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 4>), grid, blk, 0, s, ab);
     else if (planes == 3 && !a16 && t1 && epv == 2)
       hipLaunchKernelGGL((conv_glds_kernel<WM, WN, TM, TN, 3, NS, BK, M16, 2, OCC, 0, 2>), grid, blk, 0, s, ab);

@@ -44,9 +44,8 @@ static_assert(kGldsParts == 6, "one conv_glds_p<k>.hip per part");
 // The LDS-DMA configurations (see launch_mfma16); -2 when cfg is not one of them. cfg + 100: the same tile
 // with the LDS-DMA residual epilogue (epilogue_tile_rd) on the split mode's 1×1 path.
 int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
-  // cfg + 100: the slab epilogue (variants 2 / 3); cfg + 200: its direct-store form (variant 4); cfg + 300: the
-  // residual prefetched into registers (variant 5), where each applies
-  const int epv = cfg >= 300 ? 5 : cfg >= 200 ? 4 : cfg >= 100 ? 2 : 1;
+  // cfg + 100: the slab epilogue (variants 2 / 3); cfg + 200: its direct-store form (variant 4) where it applies
+  const int epv = cfg >= 200 ? 4 : cfg >= 100 ? 2 : 1;
   cfg %= 100;
   if (a.d.A2 || cfg < 11 || cfg > 65) return -2;
   return glds_part_k(cfg % kGldsParts, a, planes, cfg, s, epv);

@@ -1437,8 +1437,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
     cfg += g_glds_epv == 4 ? 200 : 100;
   // cfg + 100: the LDS-DMA residual epilogue variant; cfg + 200: its direct-store form
-  const int gc = cfg >= 311 && cfg <= 365 ? cfg - 300 : cfg >= 211 && cfg <= 265 ? cfg - 200
-               : cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;
+  const int gc = cfg >= 211 && cfg <= 265 ? cfg - 200 : cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;
   if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
