@@ -37,11 +37,9 @@ namespace {
 
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, int APL = 0>
 struct GldsCfg {
-  // BK = 64 (four k16 steps per barrier): for the bf16-row tiles (57-59, round 4); on fp32 A it measured
-  // 0.70-0.92x of the same wave tile at k32 (profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost
-  // workgroups per CU)
-  static_assert(BK == 64 || BK == 32 || BK == 16, "k per stage");
-  static_assert(BK != 64 || 64 * WM * WN >= 256, "64-deep stages: the source swizzle needs >= 256 threads");
+  // (64-deep stages were built and measured at 0.70-0.92x of the same wave tile at k32 for both operand
+  // modes, profiles/r3/bf16/ab_bk64_*.jsonl: the larger stages cost workgroups per CU; removed in round 4)
+  static_assert(BK == 32 || BK == 16, "k per stage");
   static constexpr int NT = 64 * WM * WN;
   static constexpr int BM = 32 * TM * WM;
   static constexpr int BN = 32 * TN * WN;
@@ -96,16 +94,13 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 
   // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
   // (sw16), (row >> 3) & 1 at BK = 16.
-  // BK = 64: a B row is 8 chunks (128 B), two rows per bank row, swizzle (row >> 1) & 7
-  const int cbk = BK == 64 ? (tid & 7) ^ ((tid >> 4) & 7)
-                : BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
+  const int cbk = BK == 32 ? (tid & 3) ^ (((tid >> 2) >> 2) & 3) : (tid & 1) ^ (((tid >> 1) >> 3) & 1);
   // A pieces (per plane): piece j of this thread covers tile row (j·NT + tid) / RA, LDS position
   // tid % RA, global chunk (tid % RA) ^ swzA(row) — the same for every j since NT / RA is a multiple of
   // the swizzle period. fp32 A: swzA = (row >> 1) & 7 at BK = 32, (row >> 2) & 3 at BK = 16: either way
   // the 16-lane groups of a fragment read (16 consecutive rows, one chunk) hit 16 distinct bank slots.
   // bf16 A rows: the B rows' swizzle.
   const int ca = APL ? cbk
-               : BK == 64 ? (tid & 15) ^ ((tid >> 4) & 15)
                : BK == 32 ? (tid & 7) ^ (((tid >> 3) >> 1) & 7) : (tid & 3) ^ (((tid >> 2) >> 2) & 3);
   const char* A = (APL ? reinterpret_cast<const char*>(p.A16) : reinterpret_cast<const char*>(d.A)) +
                   (int64_t)bi * p.bs_a * ES;
@@ -254,9 +249,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int brow = wn * TN * 32 + j * 32 + r;
-        const int bpos = BK == 64   ? brow * 8 + ((2 * s + h) ^ ((brow >> 1) & 7))
-                         : BK == 32 ? sw16(brow, 2 * s + h)
-                                    : brow * 2 + (h ^ ((brow >> 3) & 1));
+        const int bpos = BK == 32 ? sw16(brow, 2 * s + h) : brow * 2 + (h ^ ((brow >> 3) & 1));
 #pragma unroll
         for (int pl = 0; pl < PL; ++pl)
           fb[j][pl] = *reinterpret_cast<const bf16x8*>(st + CA + pl * CB + bpos);
@@ -266,13 +259,11 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
         const int row = wm * TM * 32 + i * 32 + r;
         bf16x8 fa[PL];
         if constexpr (APL) {
-          const int apos = BK == 64   ? row * 8 + ((2 * s + h) ^ ((row >> 1) & 7))
-                           : BK == 32 ? sw16(row, 2 * s + h)
-                                      : row * 2 + (h ^ ((row >> 3) & 1));
+          const int apos = BK == 32 ? sw16(row, 2 * s + h) : row * 2 + (h ^ ((row >> 3) & 1));
 #pragma unroll
           for (int pl = 0; pl < PL; ++pl) fa[pl] = *reinterpret_cast<const bf16x8*>(st + pl * CAP + apos);
         } else {
-        const int sz = BK == 64 ? row & 15 : BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
+        const int sz = BK == 32 ? (row >> 1) & 7 : (row >> 2) & 3;
         const int c0 = 4 * s + 2 * h;
         const float4 x0 = *reinterpret_cast<const float4*>(st + row * RA + (c0 ^ sz));
         const float4 x1 = *reinterpret_cast<const float4*>(st + row * RA + ((c0 + 1) ^ sz));
@@ -783,10 +774,7 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(53, 4, 2, 2, 2, 3, 32, true, 1, true)     /* cfg 52 on 16x16x32 MFMAs */ \
   X(54, 4, 2, 2, 2, 4, 32, true, 1, true)     /* 256×128, k32 × 4, 16x16x32 */ \
   X(55, 4, 2, 2, 4, 3, 32, true, 1, true)     /* 256×256, k32 × 3, 16x16x32 */ \
-  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */ \
-  X(57, 4, 2, 2, 2, 2, 64, false, 1, true)    /* 256×128, k64 × 2 (bf16 rows: 96 KB) */ \
-  X(58, 2, 2, 2, 2, 2, 64, false, 1, true)    /* 128×128, k64 × 2 (bf16 rows: 64 KB) */ \
-  X(59, 4, 2, 2, 2, 3, 64, false, 1, true)    /* 256×128, k64 × 3 (bf16 rows: 144 KB) */
+  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path
