@@ -52,10 +52,7 @@ bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack 
 # side with its best tile): the stage-0 1×1 expand (0.374 vs 0.401 ms) and the decoder's 9600-row
 # FFN / value / query-pos / box-head linears (1.04-1.26×). Both modes are fp32-accurate.
 _X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256, True), (256, 512, True),
-              (288, 256, True), (4, 256, False),
-              # round 4, the split kernel's direct-store 64×64 tile (214): the stage-0 reduce 1.11×, the decoder's
-              # 256×256 linears 1.17-1.26× over the fp32 MFMA (profiles/r4/x3/tune_f32_cross_r4.json)
-              (64, 256, False), (256, 256, True)}
+              (288, 256, True), (4, 256, False)}
 
 # The bf16 variant ("bf16") runs every conv and linear on bf16 operands; the stem's first conv stays on
 # the direct fp32 kernel (_direct_stem). Measured against the HF fp32 goldens (profiles/r3/bf16/, R101vd
