@@ -51,8 +51,6 @@ bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack 
 # than the fp32 MFMA at bs32 (tools/tune_conv.py --cross, profiles/r2/tune_bs32_r101vd_cross_r2.json; each
 # side with its best tile): the stage-0 1×1 expand (0.374 vs 0.401 ms) and the decoder's 9600-row
 # FFN / value / query-pos / box-head linears (1.04-1.26×). Both modes are fp32-accurate.
-DEC_POS_IN_EPILOGUE = True  # see Engine.forward's decoder loop (tools/diag/ab_modes.py measures both forms)
-
 _X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256, True), (256, 512, True),
               (288, 256, True), (4, 256, False)}
 
@@ -841,7 +839,6 @@ class Engine:
         nH, nL, nP = cfg.decoder_attention_heads, cfg.decoder_n_levels, cfg.decoder_n_points
         qp = self._buf("dec_qp", Bq, 2 * D)
         pos = self._buf("dec_pos", Bq, D)
-        hp = self._buf("dec_hp", Bq, D)
         qk = self._buf("dec_qk", Bq, 2 * D)
         vv = self._buf("dec_v", Bq, D)
         at = self._buf("dec_at", Bq, D)
@@ -849,26 +846,15 @@ class Engine:
         ff = self._buf("dec_ff", Bq, cfg.decoder_ffn_dim)
         for j, P in enumerate(self.dec):
             self._lin_op(view(ref, 4), Bq, self.qpos[0], view(qp, 2 * D), act="relu")
-            # self-attention, q = k = h + pos, v = h (M2:395-404). DEC_POS_IN_EPILOGUE: the query-pos MLP's
-            # last layer adds h in its epilogue (the same fp32 sum the A2 loader forms), so the q/k and offset
-            # projections read one operand and run on the LDS-DMA tiles (an A2 addend forces the
-            # register-staged kernel); it runs once more after the attention block for h' + pos.
-            if DEC_POS_IN_EPILOGUE:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(hp, D), res1=view(h, D))
-                self._lin_op(view(hp, D), Bq, P["qk"], view(qk, 2 * D))
-            else:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
-                self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
+            self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
+            # self-attention, q = k = h + pos, v = h (M2:395-404)
+            self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
             self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
             ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
                           (D // nH) ** -0.5)
             self._lin_op(view(at, D), Bq, P["o"], view(h, D), res1=view(h, D), ln=P["ln1"])  # in place: row-local
             # deformable cross-attention (M2:409-423)
-            if DEC_POS_IN_EPILOGUE:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(hp, D), res1=view(h, D))
-                self._lin_op(view(hp, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3))
-            else:
-                self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
+            self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
             ops.msda(V(vall, 0, L * D), j * D, view(offaw, nH * nL * nP * 3), ref, view(at, D), B, S, Q, nH,
                      D // nH, shapes, starts, nP, cfg.decoder_offset_scale)
             self._lin_op(view(at, D), Bq, P["out"], view(h, D), res1=view(h, D), ln=P["ln2"])
