@@ -565,21 +565,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
     const int oy = ty * B6_TH + wave, ox0 = tx * C3_TW;
-    // the residual rows (the basic block's shortcut) are loaded now, so their latency hides under the MFMAs
-    uint2 rq[2][2][4];
-    if (res) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ox = ox0 + j * 32 + r;
-        const bool in = oy < h && ox < w;
-        const int64_t pix = in ? ((int64_t)b * h + oy) * w + ox : 0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            rq[j][i][g] = *reinterpret_cast<const uint2*>(res + pix * ldr + i * 32 + 8 * g + 4 * hh);
-      }
-    }
     f32x16_s acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -627,7 +612,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
             const int n0 = i * 32 + 8 * g + 4 * hh;
             float rv[4] = {0.f, 0.f, 0.f, 0.f};
             if (res) {  // pre-activation residual (the basic block's shortcut), bf16 rows
-              const uint2 q = rq[j][i][g];
+              const uint2 q = *reinterpret_cast<const uint2*>(res + pix * ldr + n0);
               rv[0] = __uint_as_float(q.x << 16);
               rv[1] = __uint_as_float(q.x & 0xffff0000u);
               rv[2] = __uint_as_float(q.y << 16);
