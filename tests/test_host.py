@@ -802,3 +802,46 @@ def test_engine_refuses_fused_layernorm_on_bf16_linears():
     for prec in ("bf16", "bf16-all"):
         with pytest.raises(ValueError, match="fuse_ln"):
             Engine(PRESETS["r18vd"], {}, "cpu", precision=prec, fuse_ln=True)
+
+
+def test_merge_tile_table_keeps_entries_and_skips_winograd(tmp_path):
+    """tools/merge_tile_table.py (round 4): a measured winner beyond --min-gain replaces or adds its (shape,
+    mode) entry, a "-" win or a small gain leaves the table as it was, the Winograd component GEMMs of a
+    --detail file are skipped (wino_gemm tiles them by rule), a tile the shape cannot run (Cin % BK) is not
+    written, and every other entry keeps its comment."""
+    import json
+    import subprocess
+    import sys
+
+    table = tmp_path / "tile_table.h"
+    table.write_text("#pragma once\nconstexpr TileEntry kTileTable[] = {\n"
+                     "    {100, 256, 512, 1, 1, 3, 46},  // x1.1 keep me\n"
+                     "    {200, 128, 256, 1, 1, 3, 45},  // x1.05 replaced\n"
+                     "    {0, 0, 0, 0, 0, 0, -1},\n};\n")
+    shapes = [
+        {"m": 200, "cout": 128, "K": 256, "k": 1, "stride": 1, "mode": "x3", "times": {"-": 1.0, "46": 0.95, "247": 0.9},
+         "best_same_mode": "247"},
+        {"m": 300, "cout": 256, "K": 256, "k": 1, "stride": 1, "mode": "x3", "times": {"-": 1.0, "245": 0.99},
+         "best_same_mode": "245"},
+        {"m": 400, "cout": 256, "K": 256, "k": 1, "stride": 1, "mode": "x3", "times": {"-": 1.0, "245": 0.5},
+         "best_same_mode": "245"},
+        {"m": 500, "cout": 64, "K": 48, "k": 1, "stride": 1, "mode": "x3", "times": {"-": 1.0, "45": 0.5},
+         "best_same_mode": "45"},
+        {"m": 600, "cout": 256, "K": 256, "k": 1, "stride": 1, "mode": "x3", "times": {"-": 1.0, "246": 0.7},
+         "best_same_mode": "246"},
+    ]
+    tune = tmp_path / "tune.json"
+    tune.write_text(json.dumps({"shapes": shapes}))
+    detail = tmp_path / "detail.json"
+    detail.write_text(json.dumps([{"shape": "(400, 256, 256, 1, 1, 'x3', 'wino', 100)", "ms": 1.0, "launches": 1}]))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "merge_tile_table.py"), str(tune), "--tag", "t",
+                        "--table", str(table), "--detail", str(detail)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    src = table.read_text()
+    assert "{100, 256, 512, 1, 1, 3, 46},  // x1.1 keep me" in src
+    assert "{200, 128, 256, 1, 1, 3, 247}," in src and "replaced" not in src
+    assert "{300," not in src  # 1 % gain: below --min-gain
+    assert "{400," not in src  # a Winograd component GEMM of the detail file
+    assert "{500," not in src  # Cin 48: the LDS-DMA tile cannot run it
+    assert "{600, 256, 256, 1, 1, 3, 246}," in src
+    assert src.rstrip().endswith("};") and "{0, 0, 0, 0, 0, 0, -1}," in src

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("tunes", nargs="+")
     ap.add_argument("--tag", required=True)
     ap.add_argument("--min-gain", type=float, default=0.02)
+    ap.add_argument("--table", default=TABLE, help="the tile_table.h to update (default: the library's)")
     ap.add_argument("--detail", action="append", default=[],
                     help="bench.py --detail file: its Winograd component GEMMs (batched, tiled by wino_gemm's own "
                          "rule, not the table) are skipped")
@@ -37,7 +38,7 @@ def main():
             k = ast.literal_eval(r["shape"])
             if len(k) > 6 and k[6] == "wino":
                 wino.add(tuple(k[:3]))
-    lines = open(TABLE).read().split("\n")
+    lines = open(a.table).read().split("\n")
     ent, order = {}, []
     first = last = None
     for i, l in enumerate(lines):
@@ -68,7 +69,7 @@ def main():
     body = [f"    {{{k[0]}, {k[1]}, {k[2]}, {k[3]}, {k[4]}, {k[5]}, {v[0]}}},  {v[1]}".rstrip()
             for k, v in sorted(ent.items())]
     out = lines[:first] + body + lines[last + 1:]
-    open(TABLE, "w").write("\n".join(out))
+    open(a.table, "w").write("\n".join(out))
     for c in changed:
         print(c)
     print(f"{len(changed)} entries set; {len(ent)} in the table")
