@@ -238,6 +238,11 @@ int sp_layernorm(const float* x, int64_t ldx, const float* gamma, const float* b
 int sp_attention(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
                  int64_t ldv, float* o, int64_t ldo, int batch, int n, int heads, int dh,
                  float scale, void* stream);
+/* The same on bf16 operands (ABI v11, the bf16 variant): Q / K / V rounded to bf16 as staged, scores, softmax and
+ * accumulation in fp32; fp32 rows in and out. */
+int sp_attention_bf16(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
+                      int64_t ldv, float* o, int64_t ldo, int batch, int n, int heads, int dh,
+                      float scale, void* stream);
 int sp_msda(const sp_msda_desc* d, void* stream);
 /* Per row: top-k of x[r, 0:n] (values reduced by max over groups of `reduce_c` consecutive
  * columns first when reduce_c > 1; sigmoid applied first when apply_sigmoid), sorted by

@@ -51,6 +51,8 @@ bf16_bits = ops.bf16_bits  # fp32 → bf16 bit patterns, RNE (host, weight-pack 
 # than the fp32 MFMA at bs32 (tools/tune_conv.py --cross, profiles/r2/tune_bs32_r101vd_cross_r2.json; each
 # side with its best tile): the stage-0 1×1 expand (0.374 vs 0.401 ms) and the decoder's 9600-row
 # FFN / value / query-pos / box-head linears (1.04-1.26×). Both modes are fp32-accurate.
+ATTN_BF16 = True  # the bf16 variant's AIFI / decoder self-attention on sp_attention_bf16
+
 _X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256, True), (256, 512, True),
               (288, 256, True), (4, 256, False)}
 
@@ -191,6 +193,8 @@ class Engine:
         self.act_aifi = cfg.encoder_activation_function
         self.act_dec = cfg.decoder_activation_function
         self._conv_mode, self._lin_mode = PRECISIONS[precision]
+        # the attention core on bf16 operands where the linears around it are bf16 (sp_attention_bf16)
+        self._attn_bf16 = self._lin_mode == "bf16" and ATTN_BF16
         # bf16 conv operands: keep the backbone's activation maps in HBM as bf16 rows (half the bytes of every
         # producer write and consumer read; the GEMMs stage them as their bf16 A plane, the epilogues round
         # once at the store) instead of fp32 maps rounded per GEMM fragment. Default on for the bf16 modes.
@@ -657,7 +661,7 @@ class Engine:
         self._lin_op(view(p5, Hd), rows, A["v"], view(vv, Hd))
         heads = cfg.encoder_attention_heads
         ops.attention(V(qk, 0, 2 * Hd), V(qk, Hd, 2 * Hd), view(vv, Hd), view(at, Hd), B, n, heads, Hd // heads,
-                      (Hd // heads) ** -0.5)
+                      (Hd // heads) ** -0.5, bf16=self._attn_bf16)
         self._lin_op(view(at, Hd), rows, A["o"], view(y1, Hd), res1=view(p5, Hd), ln=A["ln1"])
         self._lin_op(view(y1, Hd), rows, A["fc1"], view(ff, cfg.encoder_ffn_dim), act=self.act_aifi)
         self._lin_op(view(ff, cfg.encoder_ffn_dim), rows, A["fc2"], view(p5a, Hd), res1=view(y1, Hd), ln=A["ln2"])
@@ -851,7 +855,7 @@ class Engine:
             self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
             self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
             ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
-                          (D // nH) ** -0.5)
+                          (D // nH) ** -0.5, bf16=self._attn_bf16)
             self._lin_op(view(at, D), Bq, P["o"], view(h, D), res1=view(h, D), ln=P["ln1"])  # in place: row-local
             # deformable cross-attention (M2:409-423)
             self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))

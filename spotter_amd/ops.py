@@ -438,13 +438,14 @@ def layernorm(x: V, gamma, beta, y: V, rows, d, eps=1e-5):
                                            stream()), 8 * rows * d, 8 * rows * d)
 
 
-def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale):
+def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale, bf16: bool = False):
+    """softmax(Q Kᵀ · scale) V; bf16: the bf16-operand kernel (sp_attention_bf16, the bf16 variant)."""
     rows = batch * n
     args = (q.need(rows, heads * dh, "attn.q"), q.ld, k.need(rows, heads * dh, "attn.k"), k.ld,
             v.need(rows, heads * dh, "attn.v"), v.ld, o.need(rows, heads * dh, "attn.o"), o.ld, batch, n, heads,
             dh, scale, stream())
-    _launch("attention", "sp_attention", args, 4 * batch * heads * n * n * dh, 16 * rows * heads * dh,
-            (batch, n, heads, dh))
+    _launch("attention", "sp_attention_bf16" if bf16 else "sp_attention", args, 4 * batch * heads * n * n * dh,
+            16 * rows * heads * dh, (batch, n, heads, dh))
 
 
 def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q, heads, head_dim,

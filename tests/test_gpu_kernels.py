@@ -856,6 +856,39 @@ def test_attention(dev, n, heads, dh):
     np.testing.assert_allclose(out.cpu().numpy().reshape(B * n, D), ref, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("n,heads,dh", [(400, 8, 32), (300, 8, 32), (1600, 8, 48), (77, 2, 64)])
+def test_attention_bf16(dev, n, heads, dh):
+    """sp_attention_bf16 (the bf16 variant's attention): Q / K / V rounded to bf16 as staged, scores, softmax and
+    accumulation in fp32, the probabilities rounded to bf16 for the P·V MFMA. Against an fp64 attention of the
+    bf16-rounded Q / K / V the only extra error is that rounding of P (2^-9 relative per term): within 1 % of
+    the output scale; against the fp32 kernel on the unrounded inputs within 3 %."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(n + dh)
+    B, D = 2, heads * dh
+    qkv = rng.standard_normal((B * n, 3 * D)).astype(np.float32)
+    t = T(qkv.reshape(-1), dev)
+    out = torch.empty(B * n * D, device=dev)
+    out32 = torch.empty(B * n * D, device=dev)
+    sc = dh ** -0.5
+    args = (V(t, 0, 3 * D), V(t, D, 3 * D), V(t, 2 * D, 3 * D))
+    ops.attention(*args, V(out, 0, D), B, n, heads, dh, sc, bf16=True)
+    ops.attention(*args, V(out32, 0, D), B, n, heads, dh, sc)
+    r16 = torch.from_numpy(qkv).to(torch.bfloat16).to(torch.float64).numpy()
+    q = r16[:, :D].reshape(B, n, heads, dh).transpose(0, 2, 1, 3)
+    k = r16[:, D:2 * D].reshape(B, n, heads, dh).transpose(0, 2, 1, 3)
+    v = r16[:, 2 * D:].reshape(B, n, heads, dh).transpose(0, 2, 1, 3)
+    s = q @ k.transpose(0, 1, 3, 2) * sc
+    s = np.exp(s - s.max(-1, keepdims=True))
+    ref = ((s / s.sum(-1, keepdims=True)) @ v).transpose(0, 2, 1, 3).reshape(B * n, D)
+    got = out.cpu().numpy().reshape(B * n, D)
+    scale = np.abs(ref).max()
+    assert np.isfinite(got).all()
+    assert np.abs(got - ref).max() <= 1e-2 * scale, np.abs(got - ref).max() / scale
+    assert np.abs(got - out32.cpu().numpy().reshape(B * n, D)).max() <= 3e-2 * scale
+
+
 def test_msda_bf16_value_rows(dev):
     """sp_msda with bf16 value rows (value_bf16, ABI v10: the bf16 variant) against the fp32-row kernel on the
     same bf16-representable values: the sampling arithmetic is fp32 either way, but the two instantiations
