@@ -815,7 +815,27 @@ def test_stem_conv_nchw(dev, case):
     np.testing.assert_allclose(got, ref, rtol=2e-4, atol=2e-4)
 
 
-@pytest.mark.parametrize("d", [256, 258, 384, 1000])  # 258: scalar path, others: float4 path
+def test_layernorm_256_rows_views(dev):
+    """The d = 256 form (four rows per wave, 16-lane groups): ragged row counts and strided row views."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(5)
+    for rows in (1, 15, 17, 1001):
+        x = (rng.standard_normal((rows, 320)) * 2 - 1).astype(np.float32)
+        g = rng.uniform(0.5, 1.5, 256).astype(np.float32)
+        b = rng.standard_normal(256).astype(np.float32)
+        y = torch.full((rows * 288,), 7.0, device=dev)
+        ops.layernorm(V(T(x.reshape(-1), dev), 32, 320), T(g, dev), T(b, dev), V(y, 0, 288), rows, 256)
+        xs = x[:, 32:288].astype(np.float64)
+        mu = xs.mean(-1, keepdims=True)
+        ref = (xs - mu) / np.sqrt(((xs - mu) ** 2).mean(-1, keepdims=True) + 1e-5) * g + b
+        got = y.cpu().numpy().reshape(rows, 288)
+        np.testing.assert_allclose(got[:, :256], ref, rtol=1e-5, atol=1e-5)
+        assert np.all(got[:, 256:] == 7.0)
+
+
+@pytest.mark.parametrize("d", [256, 258, 384, 1000])  # 258: scalar path, 256: four rows per wave, others: float4
 def test_layernorm(dev, d):
     from spotter_amd import ops
     from spotter_amd.ops import view
