@@ -843,7 +843,6 @@ class Engine:
         nH, nL, nP = cfg.decoder_attention_heads, cfg.decoder_n_levels, cfg.decoder_n_points
         qp = self._buf("dec_qp", Bq, 2 * D)
         pos = self._buf("dec_pos", Bq, D)
-        hp = self._buf("dec_hp", Bq, D)
         qk = self._buf("dec_qk", Bq, 2 * D)
         vv = self._buf("dec_v", Bq, D)
         at = self._buf("dec_at", Bq, D)
@@ -851,28 +850,15 @@ class Engine:
         ff = self._buf("dec_ff", Bq, cfg.decoder_ffn_dim)
         for j, P in enumerate(self.dec):
             self._lin_op(view(ref, 4), Bq, self.qpos[0], view(qp, 2 * D), act="relu")
-            # self-attention, q = k = h + pos, v = h (M2:395-404). bf16 linears: the query-pos MLP's last layer
-            # adds h in its epilogue (the fp32 sum the A2 loader would form), so the q/k and offset projections
-            # take one operand on the LDS-DMA tiles instead of the A2 register-staged kernel (at C3's 76800 rows
-            # 167 µs per launch); it runs once more after the attention block for h' + pos. On the fp32-accurate
-            # split the same change measured within noise, so those keep the A2 form.
-            pos_epi = self._lin_mode == "bf16" and not getattr(self, "_pos_epi_off", False)
-            if pos_epi:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(hp, D), res1=view(h, D))
-                self._lin_op(view(hp, D), Bq, P["qk"], view(qk, 2 * D))
-            else:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
-                self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
+            self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
+            # self-attention, q = k = h + pos, v = h (M2:395-404)
+            self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
             self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
             ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
                           (D // nH) ** -0.5, bf16=self._attn_bf16)
             self._lin_op(view(at, D), Bq, P["o"], view(h, D), res1=view(h, D), ln=P["ln1"])  # in place: row-local
             # deformable cross-attention (M2:409-423)
-            if pos_epi:
-                self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(hp, D), res1=view(h, D))
-                self._lin_op(view(hp, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3))
-            else:
-                self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
+            self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
             ops.msda(V(vall, 0, L * D), j * D, view(offaw, nH * nL * nP * 3), ref, view(at, D), B, S, Q, nH,
                      D // nH, shapes, starts, nP, cfg.decoder_offset_scale)
             self._lin_op(view(at, D), Bq, P["out"], view(h, D), res1=view(h, D), ln=P["ln2"])
