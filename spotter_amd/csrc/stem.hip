@@ -546,8 +546,6 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     }
   };
   if ((int64_t)blockIdx.x < ntiles) fetch(blockIdx.x);
-  const int64_t ybytes = (((int64_t)nimg * h * w - 1) * ldy + 64) * 2;
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(y, 0, (int)ybytes, 0x00020000);
   const int r = lane & 31, hh = lane >> 5;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     __syncthreads();  // the previous tile's halo reads are done
@@ -600,39 +598,36 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
       }
-    // Stores: raw buffer stores, always issued (out-of-map pixels get an offset past the buffer bound, which the
-    // hardware drops), so the store count per tile is fixed and the next tile's halo wait can leave them in
-    // flight (a data-dependent count made the compiler drain every store before the halo write).
+    if (oy < h) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ox = ox0 + j * 32 + r;
-      const bool in = oy < h && ox < w;
-      const int64_t pix = in ? ((int64_t)b * h + oy) * w + ox : 0;
+      for (int j = 0; j < 2; ++j) {
+        const int ox = ox0 + j * 32 + r;
+        if (ox >= w) continue;
+        const int64_t pix = ((int64_t)b * h + oy) * w + ox;
+        uint16_t* yrow = y + pix * ldy;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int n0 = i * 32 + 8 * g + 4 * hh;
-          float rv[4] = {0.f, 0.f, 0.f, 0.f};
-          if (res) {  // pre-activation residual (the basic block's shortcut), bf16 rows
-            const uint2 q = *reinterpret_cast<const uint2*>(res + pix * ldr + n0);
-            rv[0] = __uint_as_float(q.x << 16);
-            rv[1] = __uint_as_float(q.x & 0xffff0000u);
-            rv[2] = __uint_as_float(q.y << 16);
-            rv[3] = __uint_as_float(q.y & 0xffff0000u);
+          for (int g = 0; g < 4; ++g) {
+            const int n0 = i * 32 + 8 * g + 4 * hh;
+            float rv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (res) {  // pre-activation residual (the basic block's shortcut), bf16 rows
+              const uint2 q = *reinterpret_cast<const uint2*>(res + pix * ldr + n0);
+              rv[0] = __uint_as_float(q.x << 16);
+              rv[1] = __uint_as_float(q.x & 0xffff0000u);
+              rv[2] = __uint_as_float(q.y << 16);
+              rv[3] = __uint_as_float(q.y & 0xffff0000u);
+            }
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
+              if (res) u += rv[e];
+              v[e] = act ? fmaxf(u, 0.f) : u;
+            }
+            *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
           }
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
-            if (res) u += rv[e];
-            v[e] = act ? fmaxf(u, 0.f) : u;
-          }
-          const int off = in ? (int)((pix * ldy + n0) * 2) : 0x7ffffff8;
-          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-          const u32x2 pk = {pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(pk, yrs, off, 0, 0);
-        }
+      }
     }
   }  // tiles
 }
@@ -649,8 +644,6 @@ extern "C" int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_
                    ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 7) == 0 &&
                    (!res || (ldr >= 64 && ldr % 4 == 0 && ((uintptr_t)res & 7) == 0)),
                "sp_conv3x3_c64_bf16: bad args (act none/relu, aligned bf16 rows, ldx % 8, ldy / ldr % 4, ld >= 64)");
-  SP_ARG_CHECK((((int64_t)n * h * w - 1) * ldy + 64) * 2 < (int64_t(1) << 31) - 8,
-               "sp_conv3x3_c64_bf16: the output span must stay under 2 GiB (buffer-store offsets)");
   const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + B6_TH - 1) / B6_TH;
   const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
   const unsigned grid = (unsigned)(tiles < g_num_cus ? tiles : g_num_cus);  // persistent: one per CU

@@ -453,8 +453,7 @@ class Engine:
         if (cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw and res2 is None
                 and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
             if (self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16"
-                    and (res1 is None or res1.is_bf16) and ((n * h * w - 1) * out.ld + 64) * 2 < (1 << 31) - 8):
-                # (the kernel's buffer-store offsets cover a 2 GiB output span: bs <= 600 at 640²)
+                    and (res1 is None or res1.is_bf16)):
                 # the bf16 variant's stage-0 3x3: direct LDS-halo kernel, bit-identical to the implicit GEMM and
                 # 1.53x it at bs32 / bs256 (814 TF at C3; profiles/r3/bf16/ab_conv3x3_c64_bf16.jsonl)
                 return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act, res1=res1)
