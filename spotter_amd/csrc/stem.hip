@@ -492,17 +492,30 @@ extern "C" int sp_conv3x3_c32(const float* x, const float* wt, const float* scal
 // ---------------------------------------------------------------------------------------------
 // The stage-0 3×3 (Cin 64 → Cout 64) of the bf16 variant on bf16 rows: the Cin-32 kernel above with 64-channel
 // rows (8 chunks of 16 B, swizzled chunk ^ ((row >> 1) & 7)), all 9·64·64 bf16 weights (73.7 KB) and an
-// (8 + 2) × 66 × 64 bf16 halo (84.5 KB) in LDS, eight waves (one output row each), rows ldx / ldy elements
-// apart (the fused bottleneck tail reads this output as a channel slice). Sums the 576-deep k in (tap,
-// 16-channel) order with v_mfma_f32_32x32x16_bf16 blocks, as the implicit GEMM does.
+// (16 + 2) × (32 + 2) × 64 bf16 halo (78.3 KB) in LDS, eight waves, each two output rows × 32 pixels, rows
+// ldx / ldy elements apart (the fused bottleneck tail reads this output as a channel slice). Sums the 576-deep k
+// in (tap, 16-channel) order with v_mfma_f32_32x32x16_bf16 blocks, as the implicit GEMM does.
+// Tiles are 32 pixels wide so the 160- / 320-pixel stage-0 maps tile exactly (64-wide tiles computed 192 columns
+// of every 160). Epilogue: lanes r and r + 32 hold alternating 4-channel runs of one pixel; one
+// v_permlane32_swap per value pair gives each lane 8 consecutive channels, so the residual is read and the
+// output written as 16-byte row pieces (8 loads / stores per lane instead of 16 of 8 bytes); the residual
+// (template RES) is fetched once per tile at the start of the epilogue. At C3's shape (bs256 160², 0.48 TFLOP):
+// 0.60 / 0.71 ms without / with the residual against 0.70 / 0.91 for 64-wide tiles with 8-byte epilogue accesses
+// (profiles/r4/bf16/ab_c64_tw32.json).
+// Diagnostic build only (tools/build_diag.sh with UNIT=stem, -DSP_C64_ABL=bits): timing ablations, results wrong
+// with any bit set: 1 no output stores (nor residual use), 4 no halo loads from HBM.
+#ifndef SP_C64_ABL
+#define SP_C64_ABL 0
+#endif
 namespace sp {
 namespace {
 
-constexpr int B6_TH = 8, B6_HR = B6_TH + 2, B6_HC = C3_TW + 2;
-constexpr int B6_HALO = B6_HR * B6_HC * 8;   // 16-byte chunks of the halo
-constexpr int B6_WCH = 9 * 64 * 8;           // 16-byte chunks of the weights
+constexpr int B6_TH = 16, B6_TW = 32, B6_HR = B6_TH + 2, B6_HC = B6_TW + 2;
+constexpr int B6_HALO = B6_HR * B6_HC * 8;    // 16-byte chunks of the halo
+constexpr int B6_WCH = 9 * 64 * 8;            // 16-byte chunks of the weights
 constexpr int B6_PF = (B6_HALO + 511) / 512;  // halo chunks per thread
 
+template <bool RES>
 __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t* __restrict__ x,
                                                                   const uint16_t* __restrict__ w16,
                                                                   const float* __restrict__ scale,
@@ -533,7 +546,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
-    const int oy0 = ty * B6_TH, ox0 = tx * C3_TW;
+    const int oy0 = ty * B6_TH, ox0 = tx * B6_TW;
 #pragma unroll
     for (int k = 0; k < B6_PF; ++k) {
       const int i = tid + k * 512;
@@ -541,7 +554,11 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
       const int iy = oy0 - 1 + r, ix = ox0 - 1 + col;
       const bool ok = i < B6_HALO && (unsigned)iy < (unsigned)h && (unsigned)ix < (unsigned)w;
       const int64_t off = ok ? (((int64_t)b * h + iy) * w + ix) * ldx + c * 8 : 0;
+#if SP_C64_ABL & 4
+      pf[k] = make_uint4((unsigned)off, 0u, 0u, 0u);
+#else
       pf[k] = *reinterpret_cast<const uint4*>(x + off);
+#endif
       okm = k == 0 ? (unsigned)ok : (okm | ((unsigned)ok << k));
     }
   };
@@ -558,13 +575,30 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
       }
     }
     __syncthreads();
-    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);  // overlaps the MFMAs below
     int64_t t = tile;
     const int tx = (int)(t % tiles_x);
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
-    const int oy = ty * B6_TH + wave, ox0 = tx * C3_TW;
+    const int oy0 = ty * B6_TH + 2 * wave, ox = tx * B6_TW + r;
+    int64_t pix[2];
+    bool in[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      in[j] = oy0 + j < h && ox < w;
+      pix[j] = in[j] ? ((int64_t)b * h + oy0 + j) * w + ox : 0;
+    }
+    uint4 rq[2][2][2];  // [row j][channel half i][16-channel group p]: this lane's 8 residual channels
+    auto fetch_res = [&]() {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int p = 0; p < 2; ++p)
+            rq[j][i][p] = *reinterpret_cast<const uint4*>(res + pix[j] * ldr + i * 32 + 16 * p + 8 * hh);
+    };
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);  // overlaps the MFMAs below
     f32x16_s acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -588,8 +622,9 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
           }
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            const int col = j * 32 + r + kw;
-            fb[j] = *reinterpret_cast<const bf16x8_s*>(halo + ((wave + kh) * B6_HC + col) * 8 + f3_swz(col, ch));
+            const int col = r + kw;
+            fb[j] = *reinterpret_cast<const bf16x8_s*>(halo + ((2 * wave + j + kh) * B6_HC + col) * 8 +
+                                                       f3_swz(col, ch));
           }
 #pragma unroll
           for (int i = 0; i < 2; ++i)
@@ -598,36 +633,51 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
       }
-    if (oy < h) {
+    if constexpr (RES) fetch_res();  // issued here, not ahead of the MFMAs: 32 more live VGPRs there spill
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ox = ox0 + j * 32 + r;
-        if (ox >= w) continue;
-        const int64_t pix = ((int64_t)b * h + oy) * w + ox;
-        uint16_t* yrow = y + pix * ldy;
+    for (int j = 0; j < 2; ++j) {
+#if SP_C64_ABL & 1
+      if (!(in[j] && acc[0][j][0] == 1234.5f && acc[1][j][15] == -2.25f)) continue;
+#endif
+      uint16_t* yrow = y + pix[j] * ldy;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n0 = i * 32 + 8 * g + 4 * hh;
-            float rv[4] = {0.f, 0.f, 0.f, 0.f};
-            if (res) {  // pre-activation residual (the basic block's shortcut), bf16 rows
-              const uint2 q = *reinterpret_cast<const uint2*>(res + pix * ldr + n0);
-              rv[0] = __uint_as_float(q.x << 16);
-              rv[1] = __uint_as_float(q.x & 0xffff0000u);
-              rv[2] = __uint_as_float(q.y << 16);
-              rv[3] = __uint_as_float(q.y & 0xffff0000u);
-            }
-            float v[4];
+        for (int p = 0; p < 2; ++p) {
+          // accumulator element 4g + e of lane (r, hh) is channel i·32 + 8g + 4hh + e: swap the upper half's
+          // g = 2p run with the lower half's g = 2p + 1 run, so lane hh holds channels base .. base + 7
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                             __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+            v[e] = __uint_as_float(sw[0]);
+            v[4 + e] = __uint_as_float(sw[1]);
+          }
+          const int base = i * 32 + 16 * p + 8 * hh;
+          float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          if constexpr (RES) {  // pre-activation residual (the basic block's shortcut), bf16 rows
+            const uint4 q = rq[j][i][p];
+            const unsigned qq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[64 + n0 + e]);
-              if (res) u += rv[e];
-              v[e] = act ? fmaxf(u, 0.f) : u;
+              rv[2 * e] = __uint_as_float(qq[e] << 16);
+              rv[2 * e + 1] = __uint_as_float(qq[e] & 0xffff0000u);
             }
-            *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
           }
-      }
+          unsigned pk[4];
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            float u0 = fmaf(v[e], aff[base + e], aff[64 + base + e]);
+            float u1 = fmaf(v[e + 1], aff[base + e + 1], aff[64 + base + e + 1]);
+            if constexpr (RES) {
+              u0 += rv[e];
+              u1 += rv[e + 1];
+            }
+            pk[e / 2] = pk_bf16(act ? fmaxf(u0, 0.f) : u0, act ? fmaxf(u1, 0.f) : u1);
+          }
+          if (in[j]) *reinterpret_cast<uint4*>(yrow + base) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+        }
     }
   }  // tiles
 }
@@ -640,14 +690,18 @@ extern "C" int sp_conv3x3_c64_bf16(const uint16_t* x, int64_t ldx, const uint16_
                                    int n, int h, int w, int act, void* stream) {
   using namespace sp;
   SP_ARG_CHECK(x && w16 && scale && shift && y && n > 0 && h > 0 && w > 0 && (act == 0 || act == 1) &&
-                   ldx >= 64 && ldy >= 64 && ldx % 8 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
-                   ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 7) == 0 &&
-                   (!res || (ldr >= 64 && ldr % 4 == 0 && ((uintptr_t)res & 7) == 0)),
-               "sp_conv3x3_c64_bf16: bad args (act none/relu, aligned bf16 rows, ldx % 8, ldy / ldr % 4, ld >= 64)");
-  const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + B6_TH - 1) / B6_TH;
+                   ldx >= 64 && ldy >= 64 && ldx % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)x & 15) == 0 &&
+                   ((uintptr_t)w16 & 15) == 0 && ((uintptr_t)y & 15) == 0 &&
+                   (!res || (ldr >= 64 && ldr % 8 == 0 && ((uintptr_t)res & 15) == 0)),
+               "sp_conv3x3_c64_bf16: bad args (act none/relu, 16-byte aligned bf16 rows, ld % 8, ld >= 64)");
+  const int tiles_x = (w + B6_TW - 1) / B6_TW, tiles_y = (h + B6_TH - 1) / B6_TH;
   const int64_t tiles = (int64_t)n * tiles_x * tiles_y;
   const unsigned grid = (unsigned)(tiles < g_num_cus ? tiles : g_num_cus);  // persistent: one per CU
-  hipLaunchKernelGGL(conv3x3_c64_bf16_kernel, dim3(grid), dim3(512), 0, as_stream(stream), x, w16, scale, shift, y,
-                     ldx, ldy, res, ldr, n, h, w, tiles_x, tiles_y, act);
+  if (res)
+    hipLaunchKernelGGL(conv3x3_c64_bf16_kernel<true>, dim3(grid), dim3(512), 0, as_stream(stream), x, w16, scale,
+                       shift, y, ldx, ldy, res, ldr, n, h, w, tiles_x, tiles_y, act);
+  else
+    hipLaunchKernelGGL(conv3x3_c64_bf16_kernel<false>, dim3(grid), dim3(512), 0, as_stream(stream), x, w16, scale,
+                       shift, y, ldx, ldy, res, ldr, n, h, w, tiles_x, tiles_y, act);
   return check_launch("sp_conv3x3_c64_bf16");
 }

@@ -452,8 +452,9 @@ class Engine:
         pad = cw.k // 2
         if (cw.cin == 64 and cw.cout == 64 and cw.k == 3 and stride == 1 and not kw and res2 is None
                 and act in ("relu", None) and n * h * w >= self.C64_MIN_PIXELS):
-            if (self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16"
-                    and (res1 is None or res1.is_bf16)):
+            rows16 = lambda v: v.ld % 8 == 0 and v.off % 8 == 0  # noqa: E731 (16-byte aligned bf16 rows)
+            if (self.direct_c64_bf16 and x.is_bf16 and out.is_bf16 and cw.mode == "bf16" and rows16(x)
+                    and rows16(out) and (res1 is None or (res1.is_bf16 and rows16(res1)))):
                 # the bf16 variant's stage-0 3x3: direct LDS-halo kernel, bit-identical to the implicit GEMM and
                 # 1.53x it at bs32 / bs256 (814 TF at C3; profiles/r3/bf16/ab_conv3x3_c64_bf16.jsonl)
                 return ops.conv3x3_c64_bf16(x, cw.w16, cw.scale, cw.shift, out, n, h, w, act=act, res1=res1)

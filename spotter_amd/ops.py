@@ -367,8 +367,8 @@ def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.
                      w: int, act=None, res1: V | None = None):
     """The stage-0 3×3 of the bf16 variant (Cin 64 → 64) on bf16 rows (channel-slice views allowed): the direct
     LDS-halo kernel sp_conv3x3_c64_bf16."""
-    if not (x.is_bf16 and y.is_bf16) or x.ld % 8 or x.off % 8 or y.ld % 4 or y.off % 4:
-        raise ValueError("conv3x3_c64_bf16: aligned bf16 row views expected")
+    if not (x.is_bf16 and y.is_bf16) or x.ld % 8 or x.off % 8 or y.ld % 8 or y.off % 8:
+        raise ValueError("conv3x3_c64_bf16: 16-byte aligned bf16 row views expected")
     if w16.dtype != torch.int16 or w16.numel() != 64 * 576 or scale.numel() < 64 or shift.numel() < 64:
         raise ValueError("conv3x3_c64_bf16: weight / affine size mismatch")
     m = n * h * w
@@ -376,8 +376,8 @@ def conv3x3_c64_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.
     yp = y.need(m, 64, "c64b.y", bf16=True)
     rp, ldr = None, 0
     if res1 is not None:
-        if not res1.is_bf16 or res1.ld % 4 or res1.off % 4:
-            raise ValueError("conv3x3_c64_bf16: the residual must be 8-byte aligned bf16 rows")
+        if not res1.is_bf16 or res1.ld % 8 or res1.off % 8:
+            raise ValueError("conv3x3_c64_bf16: the residual must be 16-byte aligned bf16 rows")
         rp, ldr = res1.need(m, 64, "c64b.res", bf16=True), res1.ld
     _launch("conv", "sp_conv3x3_c64_bf16", (xp, x.ld, w16.data_ptr(), scale.data_ptr(), shift.data_ptr(), yp, y.ld,
                                             rp, ldr, n, h, w, ACT[act], stream()),
