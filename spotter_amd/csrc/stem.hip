@@ -274,15 +274,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c32_bf16_kernel(const uint16_t
 #pragma unroll
         for (int i = 0; i < TMN; ++i)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int n0 = i * 32 + 8 * g + 4 * hh;
-            float v[4];
+          for (int p = 0; p < 2; ++p) {
+            // one v_permlane32_swap per value pair gives lane hh channels base .. base + 7 (16-byte stores,
+            // as in the Cin-64 kernel below): 1.11x / 1.16x per launch at C3 (profiles/r4/bf16/ab_c32_swap.json)
+            float v[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float u = fmaf(acc[i][j][4 * g + e], aff[n0 + e], aff[CO + n0 + e]);
-              v[e] = act ? fmaxf(u, 0.f) : u;
+              const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][j][8 * p + e]),
+                                                               __float_as_uint(acc[i][j][8 * p + 4 + e]), false, false);
+              v[e] = __uint_as_float(sw[0]);
+              v[4 + e] = __uint_as_float(sw[1]);
             }
-            *reinterpret_cast<uint2*>(yrow + n0) = make_uint2(pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3]));
+            const int base = i * 32 + 16 * p + 8 * hh;
+            unsigned pk[4];
+#pragma unroll
+            for (int e = 0; e < 8; e += 2) {
+              const float u0 = fmaf(v[e], aff[base + e], aff[CO + base + e]);
+              const float u1 = fmaf(v[e + 1], aff[base + e + 1], aff[CO + base + e + 1]);
+              pk[e / 2] = pk_bf16(act ? fmaxf(u0, 0.f) : u0, act ? fmaxf(u1, 0.f) : u1);
+            }
+            *reinterpret_cast<uint4*>(yrow + base) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
           }
       }
     }
@@ -298,7 +309,7 @@ extern "C" int sp_conv3x3_c32_bf16(const uint16_t* x, const uint16_t* w16, const
   using namespace sp;
   SP_ARG_CHECK(x && w16 && scale && shift && y && n > 0 && h > 0 && w > 0 && (cout == 32 || cout == 64) &&
                    (act == 0 || act == 1) && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w16 & 15) == 0 &&
-                   ((uintptr_t)y & 7) == 0,
+                   ((uintptr_t)y & 15) == 0,
                "sp_conv3x3_c32_bf16: bad args (Cin 32, Cout 32 or 64, act none/relu, aligned dense bf16 rows)");
   constexpr int RPW = 1;
   const int tiles_x = (w + C3_TW - 1) / C3_TW, tiles_y = (h + 4 * RPW - 1) / (4 * RPW);

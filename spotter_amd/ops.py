@@ -335,7 +335,7 @@ def conv3x3_c32_bf16(x: V, w16: torch.Tensor, scale: torch.Tensor, shift: torch.
                      w: int, cout: int, act=None):
     """Stem convs 2 / 3 of the bf16 variant (RN:78-103: 3×3/1, Cin 32 → Cout 32 or 64, FrozenBN, ReLU) on dense
     bf16 NHWC rows: the direct LDS-halo kernel sp_conv3x3_c32_bf16."""
-    if not (x.is_bf16 and y.is_bf16) or x.ld != 32 or y.ld != cout:
+    if not (x.is_bf16 and y.is_bf16) or x.ld != 32 or y.ld != cout or x.off % 8 or y.off % 8:
         raise ValueError("conv3x3_c32_bf16: dense bf16 rows (ld 32 in, Cout out) expected")
     if w16.dtype != torch.int16 or w16.numel() != cout * 288 or scale.numel() < cout or shift.numel() < cout:
         raise ValueError("conv3x3_c32_bf16: weight / affine size mismatch")

@@ -41,3 +41,29 @@ for res in (False, True):
     out["res" if res else "plain"] = round(sorted(ts)[1], 4)
     out["checksum_" + ("res" if res else "plain")] = int(y.view(torch.int16).to(torch.int64).sum().item())
 print(json.dumps(out))
+
+# the stem convs 2 / 3 (Cin 32 → Cout 32 / 64) at C3's 320² map
+if os.environ.get("C32", "1") == "1":
+    n2, h2, w2 = 256, 320, 320
+    m2 = n2 * h2 * w2
+    x2 = b16(torch.randn(m2 * 32, device=dev, generator=g))
+    y2 = torch.empty(m2 * 64, dtype=torch.int16, device=dev)
+    for cout in (32, 64):
+        wt2 = b16(torch.randn(cout * 288, device=dev, generator=g) / 17)
+        def run():
+            ops.conv3x3_c32_bf16(V(x2, 0, 32), wt2, sc, sh, V(y2, 0, cout), n2, h2, w2, cout, act="relu")
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) / 10)
+        out[f"c32_{cout}"] = round(sorted(ts)[1], 4)
+        out[f"checksum_c32_{cout}"] = int(y2[:m2 * cout].to(torch.int64).sum().item())
+    print(json.dumps(out))
