@@ -33,6 +33,11 @@ __device__ unsigned long long g_glds_stamps[16384 * 6];
   } while (0)
 #endif
 
+// diagnostic A/B only: -DSP_EPI16_C8=0 keeps the bf16 slab epilogue's 8-byte store pass everywhere
+#ifndef SP_EPI16_C8
+#define SP_EPI16_C8 1
+#endif
+
 namespace {
 
 template <int WM, int WN, int TM, int TN, int PL, int NS, int BK, int APL = 0>
@@ -501,8 +506,8 @@ __device__ __forceinline__ void epilogue_tile_rdd(const ConvArgs& p, float* regi
 
 // The same slab epilogue for bf16 rows (variant 3: the bf16 variant, C_bf16 out, res1_bf16 or no residual, no
 // res2): the wave's slab (4 bytes per accumulator) holds the residual band as bf16 in its first half (LDS-DMA,
-// 16-byte pieces of 8 channels) and the rounded outputs in its second half; the store pass writes 8-byte
-// quads. Same arithmetic and rounding as epilogue_vec + store_out4: bit-identical.
+// 16-byte pieces of 8 channels) and the rounded outputs in its second half; the store pass writes 16-byte
+// pieces of 8 channels where Cout, ldc and the output base allow, else 8-byte quads. Same arithmetic and rounding as epilogue_vec + store_out4: bit-identical.
 template <int TM, int TN, int NB, bool L16>
 __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* region, f32x16 (*acc)[TN], int64_t mb,
                                                    int nb, int lane) {
@@ -529,6 +534,8 @@ __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* reg
       (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)region);
   const char* zero = reinterpret_cast<const char*>(g_zero_chunk);
   const bool res = d.res1_bf16 != nullptr;
+  const bool c8 = SP_EPI16_C8 && d.Cout % 8 == 0 && d.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(d.C_bf16) & 15) == 0 &&
+                  (d.out_rows_per_group <= 0 || d.out_group_stride % 8 == 0);
 #pragma unroll
   for (int i0 = 0; i0 < TM; i0 += NB) {
     const int64_t mr = mb + i0 * 32;
@@ -560,6 +567,19 @@ __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* reg
         }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
+    if (c8) {  // 16-byte pieces (8 channels) where every row piece is aligned and whole
+#pragma unroll 1
+      for (int t = 0; t < NQ / 2; ++t) {
+        const int cidx = lane + 64 * t;
+        const int row = cidx / (WN / 8);
+        const int col = (cidx - row * (WN / 8)) * 8;
+        const int64_t m = mr + row;
+        const int n = nb + col;
+        if (m >= p.M || n >= d.Cout) continue;
+        *reinterpret_cast<uint4*>(d.C_bf16 + out_off(d, m) + n) = *reinterpret_cast<const uint4*>(out16 + row * WN + col);
+      }
+      continue;
+    }
 #pragma unroll 1
     for (int t = 0; t < NQ; ++t) {
       const int cidx = lane + 64 * t;

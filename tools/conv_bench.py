@@ -53,6 +53,7 @@ SHAPES = [
     (256, 80, 80, 128, 128, 3, 1, "relu", False, 3),    # 28 stage1 3x3 (C3's largest bucket)
     (256, 160, 160, 64, 64, 3, 1, "relu", False, 4),    # 29 stage0 3x3
     (256, 40, 40, 256, 256, 3, 1, "relu", False, 3),    # 30 stage2 3x3
+    (1, 1, 2150400, 256, 768, 1, 1, None, False, 1),    # 31 C3 decoder value_all (3 layers x 256)
 ]
 
 
