@@ -33,9 +33,9 @@ __device__ unsigned long long g_glds_stamps[16384 * 6];
   } while (0)
 #endif
 
-// diagnostic A/B only: -DSP_EPI16_C8=0 keeps the bf16 slab epilogue's 8-byte store pass everywhere
+// -DSP_EPI16_C8=1: the bf16 slab epilogue's 16-byte store pass (built, not yet measured on the GPU; off)
 #ifndef SP_EPI16_C8
-#define SP_EPI16_C8 1
+#define SP_EPI16_C8 0
 #endif
 
 namespace {
