@@ -33,9 +33,9 @@ __device__ unsigned long long g_glds_stamps[16384 * 6];
   } while (0)
 #endif
 
-// -DSP_EPI16_C8=1: the bf16 slab epilogue's 16-byte store pass (built, not yet measured on the GPU; off)
+// the bf16 slab epilogue's 16-byte store pass (-DSP_EPI16_C8=0: the 8-byte pass everywhere, diagnostic A/B)
 #ifndef SP_EPI16_C8
-#define SP_EPI16_C8 0
+#define SP_EPI16_C8 1
 #endif
 
 namespace {
