@@ -37,6 +37,10 @@ __device__ unsigned long long g_glds_stamps[16384 * 6];
 #ifndef SP_EPI16_C8
 #define SP_EPI16_C8 1
 #endif
+// -DSP_EPI16_PAIRS=1: its LDS element pass on 4-byte column pairs (DPP swap): measured mixed, off
+#ifndef SP_EPI16_PAIRS
+#define SP_EPI16_PAIRS 0
+#endif
 
 namespace {
 
@@ -551,6 +555,34 @@ __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* reg
       glds16(src, rbase + u * 1024);
     }
     if (res) wait_vmcnt<0>();
+#if SP_EPI16_PAIRS
+    // Lanes l and l ^ 1 hold adjacent columns of the same rows, and elements q, q + 1 (q even) adjacent rows:
+    // one DPP swap per element pair gives the even lane row rr (columns cc, cc + 1) and the odd lane row rr + 1
+    // (columns cc - 1, cc), so the residual is read and the output written as 4-byte pairs.
+    const bool odd = lane & 1;
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+          const int rr = L16 ? 16 * (q >> 3) + 4 * (lane >> 4) + (q & 3) : (q & 3) + 8 * (q >> 2) + 4 * h;
+          const int cc = L16 ? 16 * ((q >> 2) & 1) + (lane & 15) : r;
+          const int k = L16 ? (q >> 2) & 1 : 0;
+          const float a0 = fmaf(acc[i0 + i][j][q], scv[j][k], shv[j][k]);
+          const float a1 = fmaf(acc[i0 + i][j][q + 1], scv[j][k], shv[j][k]);
+          const float got = __builtin_bit_cast(
+              float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, odd ? a0 : a1), 0xb1, 0xf, 0xf, false));
+          float lo = odd ? got : a0, hi = odd ? a1 : got;
+          const int pos = (i * 32 + rr + odd) * WN + j * 32 + cc - odd;
+          if (res) {
+            const uint32_t rp = *reinterpret_cast<const uint32_t*>(res16 + pos);
+            lo += bf16_lo(rp);
+            hi += bf16_lo(rp >> 16);
+          }
+          *reinterpret_cast<uint32_t*>(out16 + pos) = pack_bf16x2(act_apply(lo, d.act), act_apply(hi, d.act));
+        }
+#else
 #pragma unroll
     for (int i = 0; i < NB; ++i)
 #pragma unroll
@@ -565,6 +597,7 @@ __device__ __forceinline__ void epilogue_tile_rd16(const ConvArgs& p, float* reg
           if (res) v += bf16_lo(res16[pos]);
           out16[pos] = (uint16_t)(pack_bf16x2(act_apply(v, d.act), 0.f) & 0xffffu);
         }
+#endif
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
     if (c8) {  // 16-byte pieces (8 channels) where every row piece is aligned and whole
