@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 11
+#define SP_ABI_VERSION 12
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -300,9 +300,11 @@ typedef struct {
 int sp_jpeg_decode_coefs(const uint8_t* data, int64_t len, sp_jpeg_layout* lay, int16_t* coefs, int64_t coef_elems);
 /* Device: coefficients (device copy of the array above) → RGB: dequantise + ISLOW IDCT per 8x8 block into the
  * component planes in `work`, then fancy upsampling + YCbCr→RGB into rgb (uint8 HWC rows rgb_stride bytes
- * apart, the exact pixels Pillow's convert("RGB") produces). */
+ * apart, the exact pixels Pillow's convert("RGB") produces). status (device int32, zeroed by the caller; may
+ * be NULL) is set to 1 when a block leaves the range in which this integer IDCT and libjpeg-turbo's SIMD one
+ * agree (only corrupt or crafted coefficient data does): the caller then keeps Pillow's decode (ABI v12). */
 int sp_jpeg_to_rgb(const int16_t* coefs, const sp_jpeg_layout* lay, uint8_t* work, int64_t work_bytes, uint8_t* rgb,
-                   int64_t rgb_stride, void* stream);
+                   int64_t rgb_stride, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

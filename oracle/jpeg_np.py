@@ -53,6 +53,22 @@ def idct_islow(blocks, quant):
     return np.clip(v, 0, 255).astype(np.uint8)
 
 
+def simd_envelope_ok(coefs, lay) -> bool:
+    """Mirror of the GPU IDCT's status flag (csrc/jpeg.hip kEnv16): True when every block stays where this
+    C-semantics IDCT and libjpeg-turbo's SIMD IDCT (Pillow on x86) agree — dequantised and pass-1 values within
+    +-(2^14 - 1), pass-2 values within [-512, 511]. Files outside it are left to Pillow (tests/test_jpeg_corpus.py
+    found every divergent corrupt file outside it and no well-formed one)."""
+    env = (1 << 14) - 1
+    for c in range(lay["ncomp"]):
+        nb, off = lay["bw"][c] * lay["bh"][c], lay["block_off"][c]
+        b = coefs[off:off + nb].astype(np.int64).reshape(-1, 8, 8) * np.asarray(lay["quant"][c], np.int64).reshape(8, 8)
+        ws = _islow_1d(np.swapaxes(b, 1, 2), CB - P1)
+        out = _islow_1d(np.swapaxes(ws, 1, 2), CB + P1 + 3)
+        if np.abs(b).max() > env or np.abs(ws).max() > env or out.max() > 511 or out.min() < -512:
+            return False
+    return True
+
+
 def planes(coefs, lay):
     """Component sample planes [bh*8, bw*8] from the coefficient array and layout (dict of lists)."""
     out = []

@@ -35,16 +35,28 @@ def sources():
     return sorted(srcs, key=lambda p: not os.path.basename(p).startswith(heavy))
 
 
-def _deps_mtime():
-    hdrs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hdrs.append(os.path.join(INCLUDE, "spotter_hip.h"))
-    return max(os.path.getmtime(h) for h in hdrs)
+def _includes(path: str, seen: set) -> set:
+    """The quoted #include files a source pulls in, transitively (what its object depends on)."""
+    import re
+
+    with open(path) as f:
+        names = re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M)
+    for n in names:
+        q = os.path.normpath(os.path.join(os.path.dirname(path), n))
+        if q not in seen and os.path.exists(q):
+            seen.add(q)
+            _includes(q, seen)
+    return seen
+
+
+def _deps_mtime(src: str):
+    return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _includes(src, set())])
 
 
 def _compile(src: str, force: bool) -> str:
     obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
     if not force and os.path.exists(obj):
-        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _deps_mtime()):
+        if os.path.getmtime(obj) >= _deps_mtime(src):
             return obj
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)

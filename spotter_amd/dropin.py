@@ -3,11 +3,15 @@ time and by tests/test_dropin_reference.py in memory, so the image and the test 
 
     python -m spotter_amd.dropin <path to apps/spotter/src/spotter/serve.py>
 
-Three reference lines change: the model and processor built at import (serve.py:203-204) and the
-image open of _process_single_image (serve.py:96, `Image.open(BytesIO(image_bytes))` →
-`open_image(image_bytes)`: JPEGs decoded on the GPU, bit-identical to Pillow's pixels; other formats
-still go through Image.open). Assert-then-replace: each reference line must occur exactly once, else
-the build stops instead of shipping an image that still runs the CPU HuggingFace model.
+Only module-scope lines change; the Ray Serve deployment class AmenitiesDetector (serve.py:64-196) stays the
+reference's text byte for byte (tests/test_dropin_reference.py compares it). The model and processor built
+at import (serve.py:203-204) become the spotter_amd objects, and serve.py's module-global `Image` (bound by
+`from PIL import Image, ImageDraw`, serve.py:10) is rebound to spotter_amd.jpeg.image_module(): Pillow's
+module with a GPU `open` (JPEGs decoded on the GPU, pixels identical to Pillow's; Pillow parses the header
+first, so every file Pillow refuses raises exactly as before) whose decoded images also encode on the GPU
+in `save(..., format="JPEG")` (bytes identical to Pillow's). Assert-then-replace: each reference line must
+occur exactly once, else the build stops instead of shipping an image that still runs the CPU HuggingFace
+model.
 """
 from __future__ import annotations
 
@@ -15,14 +19,13 @@ import sys
 
 OLD_MODEL = "model = AutoModelForObjectDetection.from_pretrained(model_name).to(device)  # type: ignore"
 OLD_PROC = "processor = AutoImageProcessor.from_pretrained(model_name)"
-OLD_OPEN = "with Image.open(BytesIO(image_bytes)) as img_raw:"
 NEW_MODEL = ("from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor\n"
-             "from spotter_amd.jpeg import open_image\n"
+             "from spotter_amd.jpeg import image_module\n"
+             "Image = image_module()  # PIL.Image with the GPU JPEG decode / encode (AmenitiesDetector unchanged)\n"
              "model = SpotterForObjectDetection.from_pretrained(model_name).to(device)")
 NEW_PROC = "processor = SpotterImageProcessor.from_pretrained(model_name)"
-NEW_OPEN = "with open_image(image_bytes) as img_raw:"
 MARK = "from spotter_amd import SpotterForObjectDetection"
-REPLACEMENTS = ((OLD_MODEL, NEW_MODEL), (OLD_PROC, NEW_PROC), (OLD_OPEN, NEW_OPEN))
+REPLACEMENTS = ((OLD_MODEL, NEW_MODEL), (OLD_PROC, NEW_PROC))
 
 
 def patch_source(src: str) -> str:
@@ -40,8 +43,8 @@ def patch_source(src: str) -> str:
 
 
 def check(src: str) -> None:
-    """The patched file builds the model and processor from spotter_amd and opens images with open_image."""
-    if (MARK not in src or NEW_PROC not in src or NEW_OPEN not in src
+    """The patched file builds the model and processor from spotter_amd and rebinds Image at module scope."""
+    if (MARK not in src or NEW_PROC not in src or "Image = image_module()" not in src
             or any(old in src for old, _ in REPLACEMENTS)):
         raise ValueError("serve.py is not the spotter_amd drop-in")
 

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes as C
 import threading
+import types
 
 import numpy as np
 import torch
@@ -22,7 +23,24 @@ from ._lib import SP_JPEG_UNSUPPORTED, SpJpegLayout, lib
 
 
 class UnsupportedJpeg(ValueError):
-    """A JPEG form (or another format) the GPU decoder does not implement."""
+    """A JPEG form (or another format) the GPU decoder does not implement, or a malformed file: either way the
+    bytes go to Pillow, i.e. to the reference's own decoder and its own errors and warnings."""
+
+
+def _check_pixels(lay) -> None:
+    """Pillow's decompression-bomb rule (Image._decompression_bomb_check): above Image.MAX_IMAGE_PIXELS Pillow
+    warns, above twice that it raises DecompressionBombError. The GPU path takes neither: such a frame is left
+    to Pillow (which then warns or raises exactly as the reference does), and nothing is allocated for it."""
+    from PIL import Image
+
+    limit = Image.MAX_IMAGE_PIXELS
+    if limit is not None and max(1, lay.width) * max(1, lay.height) > limit:
+        raise UnsupportedJpeg(f"{lay.width}x{lay.height} exceeds Image.MAX_IMAGE_PIXELS: left to Pillow")
+
+
+# decode buffers a JpegDecoder keeps between calls; a larger image gets buffers of its own for that call only
+KEEP_COEFS = 1 << 25  # int16 coefficients (64 MiB pinned + 64 MiB device): a 4K 4:4:4 frame fits
+KEEP_WORK = 1 << 26   # bytes of component planes
 
 
 def _buf(data):
@@ -44,6 +62,7 @@ def decode_coefs(data, out: np.ndarray | None = None):
         raise UnsupportedJpeg(L.sp_last_error().decode(errors="replace"))
     if rc:
         raise RuntimeError(f"sp_jpeg_decode_coefs: {L.sp_last_error().decode(errors='replace')}")
+    _check_pixels(lay)
     need = lay.total_blocks * 64
     if out is None or out.size < need:
         out = np.empty(need, dtype=np.int16)
@@ -66,8 +85,9 @@ def layout_dict(lay: SpJpegLayout) -> dict:
 
 
 class JpegDecoder:
-    """Per-device decoder state: a pinned host coefficient buffer and device buffers, grown as needed and
-    reused (one decode at a time per decoder; the lock serialises concurrent callers)."""
+    """Per-device decoder state: a pinned host coefficient buffer and device buffers, grown as needed up to
+    KEEP_COEFS / KEEP_WORK and reused (one decode at a time per decoder; the lock serialises concurrent
+    callers). A larger image decodes through buffers allocated for that call and released after it."""
 
     def __init__(self, device):
         self.dev = torch.device(device)
@@ -77,16 +97,34 @@ class JpegDecoder:
         self._work = None  # device uint8 planes
         self._copied = None  # event: the last H2D copy out of the pinned buffer is done
         self._done = None  # event: the last decode's kernels are done with the device buffers
+        self._status = torch.zeros(1, dtype=torch.int32, device=self.dev)  # sp_jpeg_to_rgb's envelope flag
+        self._status_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
 
-    def _grow(self, n_coef, n_work):
-        if self._host is None or self._host.numel() < n_coef:
-            self._host = torch.empty(max(n_coef, 1 << 20), dtype=torch.int16, pin_memory=True)
-            self._coefs = torch.empty(self._host.numel(), dtype=torch.int16, device=self.dev)
-        if self._work is None or self._work.numel() < n_work:
-            self._work = torch.empty(max(n_work, 1 << 20), dtype=torch.uint8, device=self.dev)
+    def _buffers(self, n_coef, n_work):
+        """(pinned host coefficients, device coefficients, device planes, kept?) for one decode."""
+        if n_coef > KEEP_COEFS or n_work > KEEP_WORK:
+            if self._copied is not None:
+                self._copied.synchronize()
+            return (torch.empty(n_coef, dtype=torch.int16, pin_memory=True),
+                    torch.empty(n_coef, dtype=torch.int16, device=self.dev),
+                    torch.empty(n_work, dtype=torch.uint8, device=self.dev), False)
+        grow_c = self._host is None or self._host.numel() < n_coef
+        grow_w = self._work is None or self._work.numel() < n_work
+        if (grow_c or grow_w) and self._done is not None:
+            # the old buffers may still be read by the previous decode on another stream: let it finish
+            # before they go back to the caching allocator
+            self._done.synchronize()
+        if grow_c:
+            n = min(KEEP_COEFS, max(n_coef, 1 << 20))
+            self._host = torch.empty(n, dtype=torch.int16, pin_memory=True)
+            self._coefs = torch.empty(n, dtype=torch.int16, device=self.dev)
+        if grow_w:
+            self._work = torch.empty(min(KEEP_WORK, max(n_work, 1 << 20)), dtype=torch.uint8, device=self.dev)
+        return self._host, self._coefs, self._work, True
 
     def decode(self, data, out: torch.Tensor | None = None) -> torch.Tensor:
-        """JPEG bytes → uint8 [H, W, 3] on the device (on torch's current stream)."""
+        """JPEG bytes → uint8 [H, W, 3] on the device (on torch's current stream). Returns once the kernels
+        have run (the IDCT's envelope flag is read back: a file outside it raises UnsupportedJpeg, for Pillow)."""
         ptr, n, keep = _buf(data)
         lay = SpJpegLayout()
         L = lib()
@@ -96,30 +134,41 @@ class JpegDecoder:
                 raise UnsupportedJpeg(L.sp_last_error().decode(errors="replace"))
             if rc:
                 raise RuntimeError(f"sp_jpeg_decode_coefs: {L.sp_last_error().decode(errors='replace')}")
+            _check_pixels(lay)
             ncoef = lay.total_blocks * 64
-            self._grow(ncoef, lay.plane_bytes)
-            if self._copied is not None:
+            host, coefs, work, kept = self._buffers(ncoef, lay.plane_bytes)
+            if kept and self._copied is not None:
                 self._copied.synchronize()  # the pinned buffer is free again
-            rc = L.sp_jpeg_decode_coefs(ptr, n, C.byref(lay), self._host.data_ptr(), self._host.numel())
+            rc = L.sp_jpeg_decode_coefs(ptr, n, C.byref(lay), host.data_ptr(), host.numel())
             del keep
+            if rc == SP_JPEG_UNSUPPORTED:
+                raise UnsupportedJpeg(L.sp_last_error().decode(errors="replace"))
             if rc:
                 raise RuntimeError(f"sp_jpeg_decode_coefs: {L.sp_last_error().decode(errors='replace')}")
             cur = torch.cuda.current_stream(self.dev)
-            if self._done is not None:
+            if kept and self._done is not None:
                 cur.wait_event(self._done)  # another stream's previous decode may still read the buffers
-            self._coefs[:ncoef].copy_(self._host[:ncoef], non_blocking=True)
-            self._copied = torch.cuda.Event()
-            self._copied.record()
+            coefs[:ncoef].copy_(host[:ncoef], non_blocking=True)
+            copied = torch.cuda.Event()
+            copied.record()
             H, W = lay.height, lay.width
             if out is None:
                 out = torch.empty((H, W, 3), dtype=torch.uint8, device=self.dev)
             assert out.dtype == torch.uint8 and out.is_cuda and out.shape == (H, W, 3) and out.is_contiguous()
-            rc = L.sp_jpeg_to_rgb(self._coefs.data_ptr(), C.byref(lay), self._work.data_ptr(), self._work.numel(),
-                                  out.data_ptr(), W * 3, cur.cuda_stream)
+            self._status.zero_()
+            rc = L.sp_jpeg_to_rgb(coefs.data_ptr(), C.byref(lay), work.data_ptr(), work.numel(),
+                                  out.data_ptr(), W * 3, self._status.data_ptr(), cur.cuda_stream)
             if rc:
                 raise RuntimeError(f"sp_jpeg_to_rgb: {L.sp_last_error().decode(errors='replace')}")
-            self._done = torch.cuda.Event()
-            self._done.record(cur)
+            self._status_host.copy_(self._status, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(cur)
+            done.synchronize()
+            if kept:
+                self._copied, self._done = copied, done
+            if int(self._status_host[0]):
+                raise UnsupportedJpeg("coefficients outside the IDCT range shared with libjpeg-turbo's SIMD "
+                                      "code (corrupt or crafted data): left to Pillow")
             return out
 
 
@@ -136,24 +185,25 @@ def decoder(device=None) -> JpegDecoder:
         return d
 
 
-try:
-    from PIL import Image as _PILImage
-except Exception:  # pragma: no cover - Pillow is a dependency of the reference app
-    _PILImage = None
+from PIL import Image as _PILImage  # noqa: E402  (Pillow is a dependency of the reference app)
+from PIL import JpegImagePlugin as _JpegPlugin  # noqa: E402
 
 
-class DeviceRGBImage(_PILImage.Image if _PILImage is not None else object):
+class DeviceRGBImage(_PILImage.Image):
     """A PIL RGB image decoded on the GPU. `spotter_device_rgb` holds the uint8 [H, W, 3] device tensor that
     SpotterImageProcessor reads in place; the host pixels (what the unchanged draw / JPEG-encode tail of
     serve.py:119-142 needs) arrive by an async D2H copy on a side stream and are materialised only when
-    Pillow first needs them (load()). convert("RGB") / copy() of a not-yet-loaded image stay lazy."""
+    Pillow first needs them (load()). convert("RGB") / copy() of a not-yet-loaded image stay lazy. `info` is
+    the source file's, as Pillow's JpegImageFile would carry it (its "comment" is written back by save)."""
 
-    def __init__(self, rgb_dev: torch.Tensor, host=None, done=None):
+    def __init__(self, rgb_dev: torch.Tensor, host=None, done=None, info=None):
         super().__init__()
         H, W, _ = rgb_dev.shape
         self._mode = "RGB"
         self._size = (int(W), int(H))
         self.spotter_device_rgb = rgb_dev
+        if info:
+            self.info = dict(info)
         if host is None:
             dev = rgb_dev.device
             host = torch.empty(rgb_dev.shape, dtype=torch.uint8, pin_memory=True)
@@ -167,7 +217,7 @@ class DeviceRGBImage(_PILImage.Image if _PILImage is not None else object):
         self._pending = (host, done)
 
     def _lazy_copy(self):
-        return DeviceRGBImage(self.spotter_device_rgb, *self._pending)
+        return DeviceRGBImage(self.spotter_device_rgb, *self._pending, info=self.info)
 
     def load(self):
         if self._im is None and getattr(self, "_pending", None) is not None:
@@ -197,16 +247,57 @@ def _side_stream(dev):
     return s
 
 
+def _device_image(im, data, device=None):
+    """A file Pillow has opened (its header parse, identification rules and decompression-bomb check have run,
+    raising whatever the reference raises) → its GPU-decoded DeviceRGBImage, or None to keep Pillow's image:
+    other formats and modes, MPO, and every JPEG the library leaves to the host decoder."""
+    if type(im) is not _JpegPlugin.JpegImageFile or im.mode != "RGB":
+        return None
+    try:
+        return DeviceRGBImage(decoder(device).decode(data), info=im.info)
+    except UnsupportedJpeg:
+        return None
+
+
 def open_image(data, device=None):
-    """The drop-in for serve.py:96 `Image.open(BytesIO(image_bytes))`: JPEG bytes the library decodes →
-    a DeviceRGBImage (decoded on the GPU, pixels identical to Pillow's); anything else (PNG, CMYK JPEG, ...)
-    → the reference's own Image.open. Either way the caller's `.convert("RGB")` follows unchanged."""
+    """serve.py:96's `Image.open(BytesIO(image_bytes))` for raw bytes: a DeviceRGBImage for the JPEGs the
+    library decodes (pixels identical to Pillow's), Pillow's own image otherwise. Pillow parses the header
+    first, so a file Pillow refuses raises exactly what the reference raises."""
     import io
 
     b = bytes(data)
-    if len(b) >= 3 and b[:3] == b"\xff\xd8\xff":
-        try:
-            return DeviceRGBImage(decoder(device).decode(b))
-        except UnsupportedJpeg:
-            pass
-    return _PILImage.open(io.BytesIO(b))
+    im = _PILImage.open(io.BytesIO(b))
+    dev = _device_image(im, b, device)
+    if dev is None:
+        return im
+    im.close()
+    return dev
+
+
+class _ImageModule(types.ModuleType):
+    """`PIL.Image` as serve.py sees it after the drop-in: every attribute is Pillow's,
+    except `open`, which decodes JPEGs on the GPU (open_image's rule) when handed an in-memory file, as
+    serve.py:96 does. Bound at module scope, so AmenitiesDetector's body stays the reference's, byte for byte."""
+
+    def __init__(self, device=None):
+        super().__init__("PIL.Image", _PILImage.__doc__)
+        self._spotter_device = device
+
+    def __getattr__(self, name):
+        return getattr(_PILImage, name)
+
+    def open(self, fp, mode="r", formats=None):
+        import io
+
+        im = _PILImage.open(fp, mode, formats)
+        if mode == "r" and isinstance(fp, io.BytesIO):
+            dev = _device_image(im, fp.getvalue(), self._spotter_device)
+            if dev is not None:
+                im.close()
+                return dev
+        return im
+
+
+def image_module(device=None) -> types.ModuleType:
+    """The `Image` global the drop-in binds in serve.py (spotter_amd/dropin.py)."""
+    return _ImageModule(device)

@@ -102,3 +102,52 @@ def test_processor_reads_the_device_image_in_place(dev):
     mix = proc(images=[open_image(datas[0]).convert("RGB"), Image.open(io.BytesIO(datas[1])).convert("RGB")])
     ref = proc(images=[Image.open(io.BytesIO(x)).convert("RGB") for x in datas])
     assert torch.equal(mix["pixel_values"], ref["pixel_values"])
+
+
+def test_gpu_path_on_the_corrupt_corpus(dev):
+    """The ~1700 malformed files of tests/jpeg_corpus.py through the drop-in Image.open: each one either comes
+    back GPU-decoded with exactly Pillow's pixels, or is Pillow's own image (the GPU path declined: parser
+    rejection, or the IDCT kernel's status flag for coefficients outside the range shared with libjpeg-turbo's
+    SIMD code), or raises what Pillow's Image.open raises. The flag must fire on the files the oracle puts
+    outside that range."""
+    import sys
+    import warnings
+
+    sys.path.insert(0, os.path.dirname(__file__))
+    from jpeg_corpus import corpus
+
+    from oracle.jpeg_np import simd_envelope_ok
+    from spotter_amd.jpeg import DeviceRGBImage, JpegDecoder, UnsupportedJpeg, decode_coefs, image_module, layout_dict
+
+    shim = image_module(dev)
+    d = JpegDecoder(dev)
+    gpu = flagged = 0
+    for lab, data in corpus():
+        try:
+            lay, co = decode_coefs(data)
+            inside = simd_envelope_ok(co, layout_dict(lay))
+        except UnsupportedJpeg:
+            lay = None
+        if lay is not None:
+            try:
+                d.decode(data)
+                assert inside, lab
+            except UnsupportedJpeg:
+                assert not inside, lab
+                flagged += 1
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            try:
+                ref_im = Image.open(io.BytesIO(data))
+            except Exception as e:  # noqa: BLE001 - whatever Pillow raises, the shim raises too
+                with pytest.raises(type(e)):
+                    shim.open(io.BytesIO(data))
+                continue
+            im = shim.open(io.BytesIO(data))
+            if isinstance(im, DeviceRGBImage):
+                gpu += 1
+                ref = np.asarray(ref_im.convert("RGB"))
+                assert np.array_equal(np.asarray(im.convert("RGB")), ref), lab
+            else:
+                assert type(im) is type(ref_im), lab
+    assert gpu >= 100 and flagged >= 5, (gpu, flagged)

@@ -547,9 +547,9 @@ def test_dockerfile_copies_exist_in_their_contexts():
 
 
 def test_dropin_script_patches_serve_py(tmp_path):
-    """spotter_amd.dropin (run by the Dockerfile) on a copy of the reference serve.py: the lines of
-    serve.py:203-204 and the image open of serve.py:96 are replaced, a second run is a no-op, and a
-    serve.py whose lines moved is refused."""
+    """spotter_amd.dropin (run by the Dockerfile) on a copy of the reference serve.py: the module-scope lines
+    of serve.py:203-204 are replaced (plus the module-scope `Image` rebinding), a second run is a no-op, and
+    a serve.py whose lines moved is refused."""
     import sys
 
     from spotter_amd import dropin
@@ -558,7 +558,7 @@ def test_dropin_script_patches_serve_py(tmp_path):
     if os.path.exists(ref):
         src = open(ref).read()
     else:  # the GPU box has no reference: the three lines as the reference writes them
-        src = (f"import os\nmodel_name = os.environ.get('MODEL_NAME')\n            {dropin.OLD_OPEN}\n"
+        src = (f"import os\nmodel_name = os.environ.get('MODEL_NAME')\n"
                f"{dropin.OLD_MODEL}\n{dropin.OLD_PROC}\n")
     p = tmp_path / "serve.py"
     p.write_text(src)
@@ -569,7 +569,8 @@ def test_dropin_script_patches_serve_py(tmp_path):
     out = p.read_text()
     dropin.check(out)
     assert out.count("SpotterForObjectDetection.from_pretrained(model_name)") == 1
-    assert out.count("with open_image(image_bytes) as img_raw:") == 1
+    assert out.count("Image = image_module()") == 1
+    assert out.count("with Image.open(BytesIO(image_bytes)) as img_raw:") == src.count("with Image.open(")
     back = out
     for old, new in dropin.REPLACEMENTS:
         back = back.replace(new, old)
