@@ -306,6 +306,42 @@ int sp_jpeg_decode_coefs(const uint8_t* data, int64_t len, sp_jpeg_layout* lay, 
 int sp_jpeg_to_rgb(const int16_t* coefs, const sp_jpeg_layout* lay, uint8_t* work, int64_t work_bytes, uint8_t* rgb,
                    int64_t rgb_stride, int32_t* status, void* stream);
 
+/*
+ * JPEG encode (ABI v12): serve.py:139-142 `image.save(buffer, format="JPEG")`, which Pillow runs through
+ * libjpeg-turbo with quality 75 (or the caller's), 4:2:0 (or the caller's subsampling), the ISLOW forward DCT,
+ * the Annex K Huffman tables and a JFIF header. Split as the hardware wants it: colour conversion,
+ * downsampling, FDCT, quantisation and the Huffman coding itself (per-MCU bit counts, a prefix sum, then
+ * every MCU writes its bits at its own offset) on the GPU; the header bytes, the 0xFF byte stuffing and the
+ * final padding on the host. The bytes equal Pillow's (tests/test_jpeg_enc.py, tests/test_gpu_jpeg.py).
+ */
+typedef struct {
+  int32_t width, height;
+  int32_t quality;              /* 1..100 (Pillow's default -1 resolved to libjpeg's 75) */
+  int32_t h0, v0;               /* luma sampling factors (1x1, 2x1 or 2x2); chroma is 1x1 */
+  int32_t mcux, mcuy, bpm;      /* MCU grid; blocks per MCU = h0*v0 + 2 */
+  int32_t wb0, hb0;             /* luma blocks holding image data (the rest of the MCU grid: dummy blocks) */
+  int64_t total_blocks;         /* mcux * mcuy * bpm, in scan (MCU-interleaved) order */
+  int64_t work_bytes;           /* device workspace sp_jpeg_enc_rgb needs */
+  int64_t bits_cap;             /* device bytes of the entropy-coded bit buffer (worst case) */
+  uint16_t quant[2][64];        /* natural order, luma / chroma (jcparam.c jpeg_set_quality) */
+  uint16_t recip[2][64];        /* jcdctmgr.c compute_reciprocal of quant << 3: reciprocal, correction, shift */
+  uint16_t corr[2][64];
+  int16_t shift[2][64];
+} sp_jpeg_enc_layout;
+/* Host: the layout for a width x height RGB image at quality (-1 = 75) and Pillow's subsampling code (-1 or 2:
+ * 4:2:0, 1: 4:2:2, 0: 4:4:4). */
+int sp_jpeg_enc_plan(int32_t width, int32_t height, int32_t quality, int32_t subsampling, sp_jpeg_enc_layout* lay);
+/* Device: RGB pixels (uint8 rows row_stride bytes apart, pixel_bytes 3 (RGB) or 4 (RGBX)) → the entropy-coded
+ * segment, unstuffed and unpadded, MSB first, in bits[0 : ceil(*nbits / 8)); *nbits (device int64) is written.
+ * work: lay->work_bytes; bits: lay->bits_cap bytes. */
+int sp_jpeg_enc_rgb(const uint8_t* rgb, int64_t row_stride, int32_t pixel_bytes, const sp_jpeg_enc_layout* lay,
+                    uint8_t* work, int64_t work_bytes, uint8_t* bits, int64_t bits_cap, int64_t* nbits, void* stream);
+/* Host: the JPEG file: SOI, JFIF APP0, COM (comment_len > 0), DQT x2, SOF0, DHT x4, SOS, the segment with 0xFF
+ * stuffing and 1-bit padding, EOI. out_cap >= sp_jpeg_enc_max_bytes(lay, nbits, comment_len). */
+int64_t sp_jpeg_enc_max_bytes(const sp_jpeg_enc_layout* lay, int64_t nbits, int64_t comment_len);
+int sp_jpeg_enc_finish(const sp_jpeg_enc_layout* lay, const uint8_t* bits, int64_t nbits, const uint8_t* comment,
+                       int64_t comment_len, uint8_t* out, int64_t out_cap, int64_t* out_len);
+
 #ifdef __cplusplus
 }
 #endif

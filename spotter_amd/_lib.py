@@ -70,6 +70,16 @@ class SpJpegLayout(C.Structure):
     ]
 
 
+class SpJpegEncLayout(C.Structure):
+    _fields_ = [
+        ("width", i32), ("height", i32), ("quality", i32), ("h0", i32), ("v0", i32),
+        ("mcux", i32), ("mcuy", i32), ("bpm", i32), ("wb0", i32), ("hb0", i32),
+        ("total_blocks", i64), ("work_bytes", i64), ("bits_cap", i64),
+        ("quant", (C.c_uint16 * 64) * 2), ("recip", (C.c_uint16 * 64) * 2), ("corr", (C.c_uint16 * 64) * 2),
+        ("shift", (C.c_int16 * 64) * 2),
+    ]
+
+
 SP_JPEG_UNSUPPORTED = -10
 
 _SIGS = {
@@ -112,6 +122,10 @@ _SIGS = {
     "sp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp]),
     "sp_jpeg_decode_coefs": (i32, [vp, i64, C.POINTER(SpJpegLayout), vp, i64]),
     "sp_jpeg_to_rgb": (i32, [vp, C.POINTER(SpJpegLayout), vp, i64, vp, i64, vp, vp]),
+    "sp_jpeg_enc_plan": (i32, [i32, i32, i32, i32, C.POINTER(SpJpegEncLayout)]),
+    "sp_jpeg_enc_rgb": (i32, [vp, i64, i32, C.POINTER(SpJpegEncLayout), vp, i64, vp, i64, vp, vp]),
+    "sp_jpeg_enc_max_bytes": (i64, [C.POINTER(SpJpegEncLayout), i64, i64]),
+    "sp_jpeg_enc_finish": (i32, [C.POINTER(SpJpegEncLayout), vp, i64, vp, i64, vp, i64, C.POINTER(i64)]),
 }
 
 EXPORTS = tuple(_SIGS)

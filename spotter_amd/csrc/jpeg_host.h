@@ -667,5 +667,199 @@ struct Decoder {
   }
 };
 
+
+// ============================================================================================ encoder, host half
+// jcparam.c: the Annex K example tables (natural order) and the Annex K.3 Huffman tables (std_huff_tables).
+constexpr uint8_t kStdLumQ[64] = {16, 11, 10, 16, 24,  40,  51,  61,  12, 12, 14, 19, 26,  58,  60,  55,
+                                  14, 13, 16, 24, 40,  57,  69,  56,  14, 17, 22, 29, 51,  87,  80,  62,
+                                  18, 22, 37, 56, 68,  109, 103, 77,  24, 35, 55, 64, 81,  104, 113, 92,
+                                  49, 64, 78, 87, 103, 121, 120, 101, 72, 92, 95, 98, 112, 100, 103, 99};
+constexpr uint8_t kStdChrQ[64] = {17, 18, 24, 47, 99, 99, 99, 99, 18, 21, 26, 66, 99, 99, 99, 99,
+                                  24, 26, 56, 99, 99, 99, 99, 99, 47, 66, 99, 99, 99, 99, 99, 99,
+                                  99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99,
+                                  99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99, 99};
+constexpr uint8_t kDcLumBits[16] = {0, 1, 5, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+constexpr uint8_t kDcChrBits[16] = {0, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+constexpr uint8_t kDcVals[12] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
+constexpr uint8_t kAcLumBits[16] = {0, 2, 1, 3, 3, 2, 4, 3, 5, 5, 4, 4, 0, 0, 1, 0x7d};
+constexpr uint8_t kAcLumVals[162] = {
+    0x01, 0x02, 0x03, 0x00, 0x04, 0x11, 0x05, 0x12, 0x21, 0x31, 0x41, 0x06, 0x13, 0x51, 0x61, 0x07, 0x22, 0x71, 0x14,
+    0x32, 0x81, 0x91, 0xa1, 0x08, 0x23, 0x42, 0xb1, 0xc1, 0x15, 0x52, 0xd1, 0xf0, 0x24, 0x33, 0x62, 0x72, 0x82, 0x09,
+    0x0a, 0x16, 0x17, 0x18, 0x19, 0x1a, 0x25, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x34, 0x35, 0x36, 0x37, 0x38, 0x39, 0x3a,
+    0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64, 0x65,
+    0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x83, 0x84, 0x85, 0x86, 0x87, 0x88,
+    0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7, 0xa8, 0xa9,
+    0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8, 0xc9, 0xca,
+    0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe1, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9, 0xea,
+    0xf1, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+constexpr uint8_t kAcChrBits[16] = {0, 2, 1, 2, 4, 4, 3, 4, 7, 5, 4, 4, 0, 1, 2, 0x77};
+constexpr uint8_t kAcChrVals[162] = {
+    0x00, 0x01, 0x02, 0x03, 0x11, 0x04, 0x05, 0x21, 0x31, 0x06, 0x12, 0x41, 0x51, 0x07, 0x61, 0x71, 0x13, 0x22, 0x32,
+    0x81, 0x08, 0x14, 0x42, 0x91, 0xa1, 0xb1, 0xc1, 0x09, 0x23, 0x33, 0x52, 0xf0, 0x15, 0x62, 0x72, 0xd1, 0x0a, 0x16,
+    0x24, 0x34, 0xe1, 0x25, 0xf1, 0x17, 0x18, 0x19, 0x1a, 0x26, 0x27, 0x28, 0x29, 0x2a, 0x35, 0x36, 0x37, 0x38, 0x39,
+    0x3a, 0x43, 0x44, 0x45, 0x46, 0x47, 0x48, 0x49, 0x4a, 0x53, 0x54, 0x55, 0x56, 0x57, 0x58, 0x59, 0x5a, 0x63, 0x64,
+    0x65, 0x66, 0x67, 0x68, 0x69, 0x6a, 0x73, 0x74, 0x75, 0x76, 0x77, 0x78, 0x79, 0x7a, 0x82, 0x83, 0x84, 0x85, 0x86,
+    0x87, 0x88, 0x89, 0x8a, 0x92, 0x93, 0x94, 0x95, 0x96, 0x97, 0x98, 0x99, 0x9a, 0xa2, 0xa3, 0xa4, 0xa5, 0xa6, 0xa7,
+    0xa8, 0xa9, 0xaa, 0xb2, 0xb3, 0xb4, 0xb5, 0xb6, 0xb7, 0xb8, 0xb9, 0xba, 0xc2, 0xc3, 0xc4, 0xc5, 0xc6, 0xc7, 0xc8,
+    0xc9, 0xca, 0xd2, 0xd3, 0xd4, 0xd5, 0xd6, 0xd7, 0xd8, 0xd9, 0xda, 0xe2, 0xe3, 0xe4, 0xe5, 0xe6, 0xe7, 0xe8, 0xe9,
+    0xea, 0xf2, 0xf3, 0xf4, 0xf5, 0xf6, 0xf7, 0xf8, 0xf9, 0xfa};
+
+// jchuff.c jpeg_make_c_derived_tbl: symbol → (code, length); constexpr so the device tables are built at compile
+// time from the same arrays the DHT markers are written from.
+struct EncHuff {
+  uint16_t code[256];
+  uint8_t size[256];
+};
+constexpr EncHuff derive_enc(const uint8_t (&bits)[16], const uint8_t* vals) {
+  EncHuff h{};
+  int code = 0, k = 0;
+  for (int l = 1; l <= 16; ++l) {
+    for (int i = 0; i < bits[l - 1]; ++i, ++k, ++code) {
+      h.code[vals[k]] = (uint16_t)code;
+      h.size[vals[k]] = (uint8_t)l;
+    }
+    code <<= 1;
+  }
+  return h;
+}
+
+// worst case per block: DC code (<= 11 bits) + 11 magnitude bits, 63 AC codes (<= 16) + 10 magnitude bits, EOB
+constexpr int64_t kMaxBitsPerBlock = 22 + 63 * 26 + 16;
+
+inline int enc_plan(int32_t W, int32_t H, int32_t quality, int32_t subsampling, sp_jpeg_enc_layout* L) {
+  if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return -1;
+  if (quality != -1 && (quality < 1 || quality > 100)) return -1;
+  int h0, v0;
+  switch (subsampling) {  // Pillow's codes (JpegEncode.c): -1 keeps libjpeg's default 2x2
+    case -1:
+    case 2: h0 = 2; v0 = 2; break;
+    case 1: h0 = 2; v0 = 1; break;
+    case 0: h0 = 1; v0 = 1; break;
+    default: return -1;
+  }
+  memset(L, 0, sizeof(*L));
+  L->width = W;
+  L->height = H;
+  L->quality = quality == -1 ? 75 : quality;
+  L->h0 = h0;
+  L->v0 = v0;
+  L->mcux = (W + 8 * h0 - 1) / (8 * h0);
+  L->mcuy = (H + 8 * v0 - 1) / (8 * v0);
+  L->bpm = h0 * v0 + 2;
+  L->wb0 = (W + 7) / 8;
+  L->hb0 = (H + 7) / 8;
+  L->total_blocks = (int64_t)L->mcux * L->mcuy * L->bpm;
+  // jcparam.c jpeg_quality_scaling + jpeg_add_quant_table(force_baseline = TRUE)
+  const int q = L->quality;
+  const int scale = q < 50 ? 5000 / q : 200 - q * 2;
+  for (int t = 0; t < 2; ++t)
+    for (int i = 0; i < 64; ++i) {
+      long v = ((long)(t ? kStdChrQ : kStdLumQ)[i] * scale + 50L) / 100L;
+      v = v <= 0 ? 1 : (v > 255 ? 255 : v);
+      L->quant[t][i] = (uint16_t)v;
+      // jcdctmgr.c compute_reciprocal(quantval << 3) with 16-bit DCTELEM (libjpeg-turbo's SIMD build)
+      const uint32_t d = (uint32_t)v << 3;
+      uint32_t b = 0;
+      while ((d >> (b + 1)) != 0) ++b;  // flss(d) - 1
+      uint32_t r = 16 + b;
+      uint32_t fq = (1u << r) / d, fr = (1u << r) % d, c = d / 2;
+      if (fr == 0) {
+        fq >>= 1;
+        --r;
+      } else if (fr <= d / 2) {
+        ++c;
+      } else {
+        ++fq;
+      }
+      L->recip[t][i] = (uint16_t)fq;
+      L->corr[t][i] = (uint16_t)c;
+      L->shift[t][i] = (int16_t)(r - 16);
+    }
+  const int64_t nmcu = (int64_t)L->mcux * L->mcuy;
+  // device workspace: [total bits int64][per-MCU offsets int64][per-MCU bits int32][coefficients int16, 256-B aligned]
+  const int64_t coef_off = ((8 + 8 * nmcu + 4 * nmcu) + 255) / 256 * 256;
+  L->work_bytes = coef_off + L->total_blocks * 64 * 2;
+  L->bits_cap = (L->total_blocks * kMaxBitsPerBlock + 7) / 8 + 16;
+  return 0;
+}
+inline int64_t enc_coef_offset(const sp_jpeg_enc_layout& L) {
+  const int64_t nmcu = (int64_t)L.mcux * L.mcuy;
+  return ((8 + 8 * nmcu + 4 * nmcu) + 255) / 256 * 256;
+}
+
+inline int64_t enc_max_bytes(const sp_jpeg_enc_layout& L, int64_t nbits, int64_t clen) {
+  return 20 + (clen > 0 ? clen + 4 : 0) + 2 * 69 + 19 + 4 * (5 + 16) + 2 * 12 + 2 * 162 + 14 + 2 * ((nbits + 7) / 8) + 2;
+}
+
+// jcmarker.c write_file_header / write_frame_header / write_scan_header for the configuration above, Pillow's
+// COM (jpeg_write_marker after jpeg_start_compress) between them; then jchuff.c's emit_byte stuffing and
+// flush_bits padding on the segment, and EOI.
+inline int enc_finish(const sp_jpeg_enc_layout& L, const uint8_t* bits, int64_t nbits, const uint8_t* comment,
+                      int64_t clen, uint8_t* out, int64_t cap, int64_t* out_len) {
+  if (nbits < 0 || clen < 0 || clen > 65533 || cap < enc_max_bytes(L, nbits, clen)) return -1;
+  uint8_t* o = out;
+  auto b1 = [&](int v) { *o++ = (uint8_t)v; };
+  auto b2 = [&](int v) {
+    *o++ = (uint8_t)(v >> 8);
+    *o++ = (uint8_t)v;
+  };
+  b1(0xFF), b1(0xD8);
+  static const uint8_t jfif[18] = {0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0, 1, 1, 0, 0, 1, 0, 1, 0, 0};
+  memcpy(o, jfif, 18);
+  o += 18;
+  if (clen > 0) {
+    b1(0xFF), b1(0xFE), b2((int)clen + 2);
+    memcpy(o, comment, (size_t)clen);
+    o += clen;
+  }
+  for (int t = 0; t < 2; ++t) {
+    b1(0xFF), b1(0xDB), b2(67), b1(t);
+    for (int k = 0; k < 64; ++k) b1(L.quant[t][kNatural[k]]);
+  }
+  b1(0xFF), b1(0xC0), b2(17), b1(8), b2(L.height), b2(L.width), b1(3);
+  b1(1), b1((L.h0 << 4) | L.v0), b1(0);
+  b1(2), b1(0x11), b1(1);
+  b1(3), b1(0x11), b1(1);
+  struct T {
+    int idx;
+    const uint8_t* bits;
+    const uint8_t* vals;
+  } tabs[4] = {{0x00, kDcLumBits, kDcVals}, {0x10, kAcLumBits, kAcLumVals}, {0x01, kDcChrBits, kDcVals},
+               {0x11, kAcChrBits, kAcChrVals}};
+  for (const T& t : tabs) {
+    int n = 0;
+    for (int l = 0; l < 16; ++l) n += t.bits[l];
+    b1(0xFF), b1(0xC4), b2(n + 19), b1(t.idx);
+    memcpy(o, t.bits, 16);
+    o += 16;
+    memcpy(o, t.vals, (size_t)n);
+    o += n;
+  }
+  static const uint8_t sos[14] = {0xFF, 0xDA, 0x00, 0x0C, 3, 1, 0x00, 2, 0x11, 3, 0x11, 0x00, 0x3F, 0x00};
+  memcpy(o, sos, 14);
+  o += 14;
+  // the segment: whole bytes, then the last partial byte padded with 1s; every 0xFF byte followed by 0x00
+  const int64_t whole = nbits >> 3;
+  const int rest = (int)(nbits & 7);
+  const uint8_t* p = bits;
+  const uint8_t* end = bits + whole;
+  while (p < end) {
+    const uint8_t* ff = static_cast<const uint8_t*>(memchr(p, 0xFF, (size_t)(end - p)));
+    const uint8_t* stop = ff ? ff + 1 : end;
+    memcpy(o, p, (size_t)(stop - p));
+    o += stop - p;
+    if (ff) *o++ = 0x00;
+    p = stop;
+  }
+  if (rest) {
+    const uint8_t last = (uint8_t)((bits[whole] & (0xFF00 >> rest)) | (0xFF >> rest));
+    *o++ = last;
+    if (last == 0xFF) *o++ = 0x00;
+  }
+  b1(0xFF), b1(0xD9);
+  *out_len = o - out;
+  return 0;
+}
+
 }  // namespace jpeg_host
 }  // namespace sp

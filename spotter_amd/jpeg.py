@@ -19,7 +19,7 @@ import types
 import numpy as np
 import torch
 
-from ._lib import SP_JPEG_UNSUPPORTED, SpJpegLayout, lib
+from ._lib import SP_JPEG_UNSUPPORTED, SpJpegEncLayout, SpJpegLayout, lib
 
 
 class UnsupportedJpeg(ValueError):
@@ -176,6 +176,133 @@ _decoders: dict = {}
 _dec_lock = threading.Lock()
 
 
+class _ArrowArray(C.Structure):
+    pass
+
+
+_ArrowArray._fields_ = [("length", C.c_int64), ("null_count", C.c_int64), ("offset", C.c_int64),
+                        ("n_buffers", C.c_int64), ("n_children", C.c_int64), ("buffers", C.POINTER(C.c_void_p)),
+                        ("children", C.POINTER(C.POINTER(_ArrowArray))), ("dictionary", C.c_void_p),
+                        ("release", C.c_void_p), ("private_data", C.c_void_p)]
+_capsule_ptr = C.pythonapi.PyCapsule_GetPointer
+_capsule_ptr.restype = C.c_void_p
+_capsule_ptr.argtypes = [C.py_object, C.c_char_p]
+
+
+def pil_pixels(im):
+    """(host pointer, row stride, bytes per pixel, keep-alive) of a PIL RGB image's pixels: zero-copy through
+    Pillow's Arrow C-data export (RGB is stored as 4-byte RGBX pixels) when the image is one memory block, else
+    a packed RGB copy (tobytes)."""
+    im.load()
+    W, H = im.size
+    try:
+        caps = im.__arrow_c_array__()
+        arr = _ArrowArray.from_address(_capsule_ptr(caps[1], b"arrow_array"))
+        child = arr.children[0].contents
+        if arr.n_children == 1 and child.length == W * H * 4 and child.offset == 0 and arr.offset == 0:
+            return child.buffers[1], W * 4, 4, caps
+    except (AttributeError, ValueError, TypeError):
+        pass
+    b = im.tobytes()
+    return C.cast(C.c_char_p(b), C.c_void_p).value, W * 3, 3, b
+
+
+class JpegEncoder:
+    """Per-device JPEG encoder (serve.py:139-142 `image.save(buffer, format="JPEG")`): the layout per image
+    size / quality / subsampling, device workspace and bit buffer, pinned staging for the pixel upload and the
+    bit download, all grown as needed and reused (one encode at a time; the lock serialises callers)."""
+
+    def __init__(self, device):
+        self.dev = torch.device(device)
+        self._lock = threading.Lock()
+        self._plans: dict = {}
+        self._work = self._bits = self._pix = None
+        self._stage = self._down = None
+        self._nbits = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self._nbits_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+
+    def plan(self, W, H, quality=-1, subsampling=-1) -> SpJpegEncLayout:
+        key = (W, H, quality, subsampling)
+        lay = self._plans.get(key)
+        if lay is None:
+            lay = SpJpegEncLayout()
+            if lib().sp_jpeg_enc_plan(W, H, quality, subsampling, C.byref(lay)):
+                raise ValueError(lib().sp_last_error().decode(errors="replace"))
+            if len(self._plans) > 64:
+                self._plans.clear()
+            self._plans[key] = lay
+        return lay
+
+    @staticmethod
+    def _grow(t, n, dtype, device=None, pinned=False):
+        if t is not None and t.numel() >= n:
+            return t
+        n = max(n, 1 << 20)
+        if pinned:
+            return torch.empty(n, dtype=dtype, pin_memory=True)
+        return torch.empty(n, dtype=dtype, device=device)
+
+    def encode(self, src, quality=-1, subsampling=-1, comment: bytes | None = None) -> bytes:
+        """src: a uint8 [H, W, 3] device tensor, or a PIL RGB image (its host pixels are uploaded)."""
+        with self._lock:
+            L = lib()
+            cur = torch.cuda.current_stream(self.dev)
+            if isinstance(src, torch.Tensor):
+                assert src.dtype == torch.uint8 and src.is_cuda and src.dim() == 3 and src.shape[2] in (3, 4)
+                assert src.stride(2) == 1 and src.stride(1) == src.shape[2]
+                H, W, pb = src.shape
+                ptr, stride, keep = src.data_ptr(), src.stride(0), src
+            else:
+                W, H = src.size
+                hptr, stride, pb, keep_h = pil_pixels(src)
+                n = stride * H
+                self._stage = self._grow(self._stage, n, torch.uint8, pinned=True)
+                self._pix = self._grow(self._pix, n, torch.uint8, self.dev)
+                C.memmove(self._stage.data_ptr(), hptr, n)
+                del keep_h
+                self._pix[:n].copy_(self._stage[:n], non_blocking=True)
+                ptr, keep = self._pix.data_ptr(), None
+            lay = self.plan(W, H, quality, subsampling)
+            self._work = self._grow(self._work, lay.work_bytes, torch.uint8, self.dev)
+            self._bits = self._grow(self._bits, lay.bits_cap, torch.uint8, self.dev)
+            rc = L.sp_jpeg_enc_rgb(ptr, stride, pb, C.byref(lay), self._work.data_ptr(), self._work.numel(),
+                                   self._bits.data_ptr(), self._bits.numel(), self._nbits.data_ptr(), cur.cuda_stream)
+            if rc:
+                raise RuntimeError(f"sp_jpeg_enc_rgb: {L.sp_last_error().decode(errors='replace')}")
+            self._nbits_host.copy_(self._nbits, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            ev.synchronize()
+            nbits = int(self._nbits_host[0])
+            nbytes = (nbits + 7) // 8
+            self._down = self._grow(self._down, nbytes, torch.uint8, pinned=True)
+            self._down[:nbytes].copy_(self._bits[:nbytes], non_blocking=True)
+            ev.record(cur)
+            ev.synchronize()
+            del keep
+            com = comment or b""
+            cap = L.sp_jpeg_enc_max_bytes(C.byref(lay), nbits, len(com))
+            out = C.create_string_buffer(cap)
+            n = C.c_int64()
+            rc = L.sp_jpeg_enc_finish(C.byref(lay), self._down.data_ptr(), nbits, com, len(com), out, cap,
+                                      C.byref(n))
+            if rc:
+                raise RuntimeError(f"sp_jpeg_enc_finish: {L.sp_last_error().decode(errors='replace')}")
+            return out.raw[:n.value]
+
+
+_encoders: dict = {}
+
+
+def encoder(device=None) -> JpegEncoder:
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    with _dec_lock:
+        e = _encoders.get(dev)
+        if e is None:
+            e = _encoders[dev] = JpegEncoder(dev)
+        return e
+
+
 def decoder(device=None) -> JpegDecoder:
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     with _dec_lock:
@@ -235,6 +362,40 @@ class DeviceRGBImage(_PILImage.Image):
         if self._im is None:
             return self._lazy_copy()
         return super().copy()
+
+    def save(self, fp, format=None, **params):
+        """serve.py:140 `image.save(buffer, format="JPEG")`: encoded on the GPU, the bytes Pillow writes. An image
+        whose pixels never reached the host encodes from its device copy; once loaded (drawn on), its host
+        pixels are uploaded. Other formats, file names and options go to Pillow's own save."""
+        opts = _gpu_jpeg_options(self, fp, format, params)
+        if opts is None:
+            return super().save(fp, format, **params)
+        src = self.spotter_device_rgb if self._im is None else self
+        fp.write(encoder(self.spotter_device_rgb.device).encode(src, *opts))
+
+
+_SUBSAMPLING = {-1: -1, 0: 0, 1: 1, 2: 2, "4:4:4": 0, "4:2:2": 1, "4:2:0": 2, "4:1:1": 2}
+
+
+def _gpu_jpeg_options(im, fp, format, params):
+    """(quality, subsampling, comment) when Pillow's JPEG save of `im` with these arguments is what the GPU
+    encoder writes (JpegImagePlugin._save: baseline, standard tables, no dpi / EXIF / ICC / XMP / extra,
+    comment from im.info), else None."""
+    if format is None or str(format).upper() not in ("JPEG", "JPG") or not hasattr(fp, "write"):
+        return None
+    if im.mode != "RGB" or set(params) - {"quality", "subsampling"}:
+        return None
+    q = params.get("quality", -1)
+    sub = params.get("subsampling", -1)
+    if type(q) is not int or not (q == -1 or 1 <= q <= 100):
+        return None
+    if not isinstance(sub, (int, str)) or sub not in _SUBSAMPLING:
+        return None
+    comment = im.info.get("comment")
+    if comment is not None and (not isinstance(comment, bytes) or len(comment) > 65533):
+        return None
+    # (dpi, EXIF, ICC and XMP come from the save() arguments only, never from im.info: any of them → Pillow)
+    return q, _SUBSAMPLING[sub], comment
 
 
 _sides: dict = {}

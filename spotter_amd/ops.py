@@ -444,8 +444,9 @@ def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale, bf16: bool = F
     args = (q.need(rows, heads * dh, "attn.q"), q.ld, k.need(rows, heads * dh, "attn.k"), k.ld,
             v.need(rows, heads * dh, "attn.v"), v.ld, o.need(rows, heads * dh, "attn.o"), o.ld, batch, n, heads,
             dh, scale, stream())
-    _launch("attention", "sp_attention_bf16" if bf16 else "sp_attention", args, 4 * batch * heads * n * n * dh,
-            16 * rows * heads * dh, (batch, n, heads, dh))
+    # the bf16-operand kernel is its own class, priced at the bf16 MFMA peak (bench.py CLASS_BOUND)
+    _launch("attention_bf16" if bf16 else "attention", "sp_attention_bf16" if bf16 else "sp_attention", args,
+            4 * batch * heads * n * n * dh, 16 * rows * heads * dh, (batch, n, heads, dh))
 
 
 def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q, heads, head_dim,

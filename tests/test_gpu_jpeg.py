@@ -73,9 +73,10 @@ def test_open_image_is_a_lazy_pil_image(dev):
         for d in (d1, d2):
             d.rectangle([10, 10, 200, 100], outline="red", width=3)
         assert np.array_equal(np.asarray(im), np.asarray(ref))
-        b = io.BytesIO()
-        im.save(b, format="JPEG")
-        assert b.getvalue()[:2] == b"\xff\xd8"
+        b, b2 = io.BytesIO(), io.BytesIO()
+        im.save(b, format="JPEG")  # drawn on: the host pixels go up to the GPU encoder
+        ref.save(b2, format="JPEG")
+        assert b.getvalue() == b2.getvalue()
     p = io.BytesIO()
     ref.save(p, "PNG")
     other = open_image(p.getvalue())
@@ -151,3 +152,74 @@ def test_gpu_path_on_the_corrupt_corpus(dev):
             else:
                 assert type(im) is type(ref_im), lab
     assert gpu >= 100 and flagged >= 5, (gpu, flagged)
+
+
+def _pillow_jpeg(img, comment=None, **kw):
+    im = Image.fromarray(img)
+    if comment:
+        im.info["comment"] = comment
+    b = io.BytesIO()
+    im.save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def test_gpu_encode_writes_pillows_bytes(dev):
+    """sp_jpeg_enc_rgb + the host finish against Pillow's own save, byte for byte: the reference fixture decoded
+    (what serve.py re-encodes), synthetic 640², 720p and 1080p frames, odd sizes (dummy blocks), noise, every
+    subsampling, qualities 1..100, a comment; from a device tensor (RGB) and from host pixels (RGBX / RGB)."""
+    from spotter_amd.jpeg import JpegEncoder
+    from spotter_amd.synthetic import synthetic_image
+
+    enc = JpegEncoder(dev)
+    ref_img = np.asarray(Image.open(GOLDEN).convert("RGB"))
+    cases = [("test_pic", ref_img, {}), ("640", synthetic_image(1, 640, 640), {}),
+             ("720p", synthetic_image(2, 720, 1280), {}), ("1080p", synthetic_image(3, 1080, 1920), {})]
+    rng = np.random.default_rng(0)
+    for (h, w) in [(1, 1), (2, 3), (9, 17), (17, 33), (31, 2), (123, 77), (233, 177)]:
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8) if min(h, w) < 4 else synthetic_image(h + w, h, w)
+        for q in (-1, 1, 50, 100):
+            for sub in (-1, 0, 1, 2):
+                cases.append((f"{h}x{w} q{q} s{sub}", img, {"quality": q, "subsampling": sub}))
+    noise = rng.integers(0, 256, (96, 80, 3), dtype=np.uint8)
+    cases += [("noise q100", noise, {"quality": 100}), ("noise q1", noise, {"quality": 1})]
+    for name, img, kw in cases:
+        pkw = {k: v for k, v in kw.items() if v != -1}
+        want = _pillow_jpeg(img, **pkw)
+        t = torch.from_numpy(np.ascontiguousarray(img)).to(dev)
+        got = enc.encode(t, kw.get("quality", -1), kw.get("subsampling", -1))
+        assert got == want, f"{name}: {len(got)} vs {len(want)} bytes"
+        if name in ("test_pic", "640") or "q-1 s-1" in name:
+            assert enc.encode(Image.fromarray(img)) == want, name  # host pixels (Arrow RGBX or packed RGB)
+    img = synthetic_image(9, 50, 60)
+    t = torch.from_numpy(img).to(dev)
+    assert enc.encode(t, comment=b"spotter") == _pillow_jpeg(img, comment=b"spotter")
+    big = Image.fromarray(synthetic_image(5, 2160, 3840))  # several Pillow memory blocks: packed-RGB upload
+    assert enc.encode(big) == _pillow_jpeg(np.asarray(big))
+
+
+def test_serve_tail_with_the_drop_in_image_module(dev):
+    """serve.py:96-142 as the unchanged class runs it after the drop-in: Image.open (module shim) → convert →
+    draw → save(format="JPEG") → base64 gives the reference's exact base64 string; without a draw the encoder
+    reads the device copy (no host pixels pulled)."""
+    import base64
+
+    from spotter_amd.jpeg import DeviceRGBImage, image_module
+
+    Img = image_module(dev)
+    data = open(GOLDEN, "rb").read()
+    for draw in (True, False):
+        with Img.open(io.BytesIO(data)) as raw, Image.open(io.BytesIO(data)) as raw_ref:
+            image, ref = raw.convert("RGB"), raw_ref.convert("RGB")
+            assert isinstance(image, DeviceRGBImage)
+            if draw:
+                for im in (image, ref):
+                    d = ImageDraw.Draw(im)
+                    d.rectangle([100.5, 80.25, 400.75, 300.0], outline="red", width=3)
+                    d.text(xy=(105.5, 85.25), text="dining area", fill="white", stroke_width=1, stroke_fill="black")
+            outs = []
+            for im in (image, ref):
+                b = io.BytesIO()
+                im.save(b, format="JPEG")
+                outs.append(base64.b64encode(b.getvalue()).decode("utf-8"))
+            assert outs[0] == outs[1]
+            assert (getattr(image, "_im", None) is None) == (not draw)

@@ -66,14 +66,15 @@ def serve_bytes(payload: bytes):
 
 
 def opener(decode: str):
-    """serve.py:96's image open: the drop-in's open_image (GPU JPEG decode) or, with
-    decode="host", the reference's own Image.open."""
+    """serve.py:96's `Image.open(BytesIO(image_bytes))`: through the drop-in's module-scope `Image`
+    (spotter_amd.jpeg.image_module(): GPU JPEG decode, and GPU JPEG encode in the later save)
+    or, with decode="host", the reference's own PIL.Image (host decode and host encode)."""
     if decode == "gpu":
-        from spotter_amd.jpeg import open_image
+        from spotter_amd.jpeg import image_module
 
-        return open_image
-    from PIL import Image
-
+        Image = image_module()
+    else:
+        from PIL import Image
     return lambda data: Image.open(io.BytesIO(data))
 
 
@@ -107,12 +108,15 @@ async def process_image(client, url, proc, model, stamps, open_fn=None):
             draw.text(xy=(box[0] + 5, box[1] + 5), text=AMENITIES[label], fill="white", stroke_width=1,
                       stroke_fill="black")
             found.append({"label": AMENITIES[label], "box": box})
+        t3b = time.perf_counter()
         buf = io.BytesIO()
         image.save(buf, format="JPEG")
         b64 = base64.b64encode(buf.getvalue()).decode("utf-8")
         t4 = time.perf_counter()
-    for k, a, b in (("fetch", t0, t1), ("decode", t1, t2), ("detect", t2, t3), ("draw_jpeg_b64", t3, t4)):
+    for k, a, b in (("fetch", t0, t1), ("decode", t1, t2), ("detect", t2, t3), ("draw_jpeg_b64", t3, t4),
+                    ("draw", t3, t3b), ("jpeg_b64", t3b, t4)):
         stamps.setdefault(k, []).append((b - a) * 1e3)
+    stamps.setdefault("n_drawn", []).append(len(found))
     return {"url": url, "detections": found, "labeled_image_base64": b64}
 
 

@@ -16,9 +16,10 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce", "stem_conv", "conv3x3")), ("msda", ("msda",)), ("attention", ("attn_",)),
+CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "splitk_reduce", "stem_conv", "conv3x3")), ("msda", ("msda",)),
+           ("attention_bf16", ("attn_bf16",)), ("attention", ("attn_",)),
            ("preprocess", ("preprocess",)), ("topk", ("topk",)), ("layernorm", ("layernorm",))]
-LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_", "preprocess": None, "topk": "topk",
+LEADERS = {"conv": "conv_", "msda": "msda", "attention": "attn_mfma", "attention_bf16": "attn_bf16", "preprocess": None, "topk": "topk",
            "layernorm": "layernorm"}
 
 

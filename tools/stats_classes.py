@@ -10,7 +10,7 @@ import os
 import sys
 
 CLASSES = [("conv", ("conv_gemm", "conv_mfma16", "conv_glds", "conv_pipe", "stem_conv", "conv3x3")), ("conv_splitk_reduce", ("splitk_reduce",)), ("msda", ("msda",)),
-           ("attention", ("attn_",)), ("preprocess", ("preprocess",)), ("topk", ("topk",)),
+           ("attention_bf16", ("attn_bf16",)), ("attention", ("attn_",)), ("preprocess", ("preprocess",)), ("topk", ("topk",)),
            ("layernorm", ("layernorm",)), ("postprocess_decode", ("decode_kernel",)), ("wino_tf", ("wino_",))]
 
 
