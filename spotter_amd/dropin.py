@@ -9,7 +9,9 @@ at import (serve.py:203-204) become the spotter_amd objects, and serve.py's modu
 `from PIL import Image, ImageDraw`, serve.py:10) is rebound to spotter_amd.jpeg.image_module(): Pillow's
 module with a GPU `open` (JPEGs decoded on the GPU, pixels identical to Pillow's; Pillow parses the header
 first, so every file Pillow refuses raises exactly as before) whose decoded images also encode on the GPU
-in `save(..., format="JPEG")` (bytes identical to Pillow's). Assert-then-replace: each reference line must
+in `save(..., format="JPEG")` (bytes identical to Pillow's); `ImageDraw` is rebound to
+spotter_amd.draw.draw_module() (Pillow's ImageDraw, the default font's glyph masks memoised: Pillow's
+pixels). Assert-then-replace: each reference line must
 occur exactly once, else the build stops instead of shipping an image that still runs the CPU HuggingFace
 model.
 """
@@ -20,8 +22,10 @@ import sys
 OLD_MODEL = "model = AutoModelForObjectDetection.from_pretrained(model_name).to(device)  # type: ignore"
 OLD_PROC = "processor = AutoImageProcessor.from_pretrained(model_name)"
 NEW_MODEL = ("from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor\n"
+             "from spotter_amd.draw import draw_module\n"
              "from spotter_amd.jpeg import image_module\n"
              "Image = image_module()  # PIL.Image with the GPU JPEG decode / encode (AmenitiesDetector unchanged)\n"
+             "ImageDraw = draw_module()  # PIL.ImageDraw whose default font memoises its glyph masks\n"
              "model = SpotterForObjectDetection.from_pretrained(model_name).to(device)")
 NEW_PROC = "processor = SpotterImageProcessor.from_pretrained(model_name)"
 MARK = "from spotter_amd import SpotterForObjectDetection"
@@ -45,6 +49,7 @@ def patch_source(src: str) -> str:
 def check(src: str) -> None:
     """The patched file builds the model and processor from spotter_amd and rebinds Image at module scope."""
     if (MARK not in src or NEW_PROC not in src or "Image = image_module()" not in src
+            or "ImageDraw = draw_module()" not in src
             or any(old in src for old, _ in REPLACEMENTS)):
         raise ValueError("serve.py is not the spotter_amd drop-in")
 

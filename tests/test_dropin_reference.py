@@ -120,7 +120,9 @@ def test_deployment_class_is_byte_identical_to_the_reference(monkeypatch, tmp_pa
     assert inspect.getsource(cls) == ref_text
     from spotter_amd.jpeg import _ImageModule
 
-    assert isinstance(serve.Image, _ImageModule) and serve.ImageDraw.__name__ == "PIL.ImageDraw"
+    from spotter_amd.draw import _DrawModule
+
+    assert isinstance(serve.Image, _ImageModule) and isinstance(serve.ImageDraw, _DrawModule)
 
 
 def test_reference_deployment_module_binds_our_objects(monkeypatch, tmp_path):

@@ -36,7 +36,7 @@ def test_weights_are_deterministic():
 
 def _header_functions():
     src = open(os.path.join(ROOT, "include", "spotter_hip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(sp_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(sp_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_header_symbol():

@@ -66,24 +66,25 @@ def serve_bytes(payload: bytes):
 
 
 def opener(decode: str):
-    """serve.py:96's `Image.open(BytesIO(image_bytes))`: through the drop-in's module-scope `Image`
-    (spotter_amd.jpeg.image_module(): GPU JPEG decode, and GPU JPEG encode in the later save)
-    or, with decode="host", the reference's own PIL.Image (host decode and host encode)."""
+    """(serve.py:96's `Image.open(BytesIO(image_bytes))`, serve.py:119's `ImageDraw`): the drop-in's module-scope
+    `Image` (spotter_amd.jpeg.image_module(): GPU JPEG decode, and GPU JPEG encode in the later save) and
+    `ImageDraw` (spotter_amd.draw.draw_module()); or, with decode="host", the reference's own
+    PIL modules (host decode, Pillow draw and encode)."""
     if decode == "gpu":
+        from spotter_amd.draw import draw_module
         from spotter_amd.jpeg import image_module
 
-        Image = image_module()
+        Image, ImageDraw = image_module(), draw_module()
     else:
-        from PIL import Image
-    return lambda data: Image.open(io.BytesIO(data))
+        from PIL import Image, ImageDraw
+    return (lambda data: Image.open(io.BytesIO(data))), ImageDraw
 
 
 async def process_image(client, url, proc, model, stamps, open_fn=None):
     """One image of a /detect request (serve.py:79-148 order), with per-stage time stamps."""
     import torch
-    from PIL import ImageDraw
 
-    open_fn = open_fn or opener("gpu")
+    open_fn, ImageDraw = open_fn or opener("gpu")
     t0 = time.perf_counter()
     r = await client.get(url)
     r.raise_for_status()
