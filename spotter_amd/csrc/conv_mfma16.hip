@@ -289,6 +289,13 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
 __device__ unsigned long long g_x3s_stamps[8 * 64 * 8];
 #endif
 
+// The software-pipelined (conv_pipe, cfg 21-26) and ping-pong (conv_pp, cfg 31-32) kernels below measured slower
+// than the LDS-DMA tiles on every C2 / C3 / C5 shape and are in no tile table: diagnostic builds only
+// (UNIT=conv_mfma16 tools/build_diag.sh <name> -DSP_DIAG_KERNELS=1), not the product library.
+#ifndef SP_DIAG_KERNELS
+#define SP_DIAG_KERNELS 0
+#endif
+#if SP_DIAG_KERNELS
 // ---------------------------------------------------------------------------------------------
 // Software-pipelined LDS-DMA variant: as conv_glds_kernel, plus the fragment loads (ds_read +
 // bf16 split) of k16 step t+1 are issued between the MFMAs of step t (sched_group_barrier
@@ -747,6 +754,7 @@ int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
 }
 
 
+#endif  // SP_DIAG_KERNELS
 // ---------------------------------------------------------------------------------------------
 // Staggered split-GEMM kernel (x3 / bf16): 8 waves, each owning 32 rows × the whole BN = 32·TN
 // columns of a 256 × BN tile, so every A fragment is split once per workgroup (VALU per MFMA
@@ -1411,6 +1419,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_x3s<4>(a, planes, s);  // 256×128
     }
   }
+#if SP_DIAG_KERNELS
   if (cfg >= 31 && cfg <= 32 && !a.d.A2) {
     switch (cfg) {
       case 31: return launch_pp<2, 2>(a, planes, s);  // 256×128, waves of 64×64
@@ -1427,6 +1436,12 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_pipe<2, 2, 2, 1, 4>(a, planes, s);   // 128×64, 4 stages
     }
   }
+#else
+  if (((cfg >= 31 && cfg <= 32) || (cfg >= 21 && cfg <= 26)) && !a.d.A2) {
+    set_error("sp_conv2d: tile configuration %d (conv_pipe / conv_pp) is in the diagnostic build only", cfg);
+    return -1;
+  }
+#endif
   // The slab epilogue (conv_glds.h epilogue_tile_rd, "cfg + 100") on the split mode's launches with a BN affine
   // or a residual, for the tiles where it measured faster, bit-identical either way: 1.02-1.28x on the
   // bottleneck expands (the res1 band fetched by LDS-DMA; profiles/r3/x3/ab_residual_dma_epilogue.jsonl),

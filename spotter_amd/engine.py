@@ -165,8 +165,8 @@ class Engine:
         # post-norm LayerNorms in the preceding GEMM's epilogue (_lin_op ln=). Off by default: the fused
         # kernel needs whole rows per workgroup (32-row fp32-MFMA tiles), which at bs32 ran the 21 GEMMs at
         # 42 TF/s (2.47 ms/step) against 1.4 ms/step for the unfused GEMMs + 21 sp_layernorm launches
-        # (profiles/r2/fused_ln_ab.json); it stays selectable and tested.
-        self.fuse_ln = fuse_ln
+        # (profiles/r2/fused_ln_ab.json); it stays selectable, in diagnostic library builds (SP_DIAG_KERNELS).
+        self.fuse_ln = fuse_ln  # the fused-LN epilogue is compiled into diagnostic library builds only
         if fuse_ln and PRECISIONS.get(precision, ("", ""))[1] == "bf16":
             # the fused-LN tile runs fp32 weights: it would silently raise the bf16 linears' operand precision
             raise ValueError(f"fuse_ln=True runs the linears on fp32 weights: not available with precision={precision!r}")

@@ -1085,6 +1085,8 @@ def test_rowmax(dev, rows, c, ld):
     np.testing.assert_array_equal(out.cpu().numpy(), x[:, :c].max(1))
 
 
+@pytest.mark.skipif("_diag" not in os.environ.get("SPOTTER_HIP_LIB", ""),
+                    reason="the fused LayerNorm epilogue is in diagnostic builds only (SP_DIAG_KERNELS)")
 @pytest.mark.parametrize("rows,k,n", [(1, 256, 256), (37, 1024, 256), (9600, 256, 256), (130, 384, 384),
                                       (64, 2048, 384), (33, 256, 512)])
 def test_linear_fused_layernorm(dev, rows, k, n):
