@@ -726,9 +726,11 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   // a tile whose stages do not fit the 160 KB LDS for this operand mode is not instantiated
   using C3 = GldsCfg<WM, WN, TM, TN, 3, NS, BK>;
   using C1 = GldsCfg<WM, WN, TM, TN, 1, NS, BK>;
-  using C1a = GldsCfg<WM, WN, TM, TN, 1, NS, BK, 1>;
   constexpr bool fit3 = C3::SMEM * 16 <= 163840, fit1 = C1::SMEM * 16 <= 163840;
-  constexpr bool fit1a = AB && C1a::SMEM * 16 <= 163840;  // bf16 A rows: the bf16 operand mode only
+  constexpr bool fit1a = [] {  // bf16 A rows: the bf16 operand mode only (not instantiated unless AB)
+    if constexpr (AB) return GldsCfg<WM, WN, TM, TN, 1, NS, BK, 1>::SMEM * 16 <= 163840;
+    else return false;
+  }();
   const bool a16 = a.A16 != nullptr;
   if (a16 && (planes == 3 || !fit1a)) return -2;  // no bf16-A form of this tile: the caller picks another
   if ((planes == 3 && !fit3) || (planes != 3 && !(a16 ? fit1a : fit1))) {
@@ -827,7 +829,12 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(53, 4, 2, 2, 2, 3, 32, true, 1, true)     /* cfg 52 on 16x16x32 MFMAs */ \
   X(54, 4, 2, 2, 2, 4, 32, true, 1, true)     /* 256×128, k32 × 4, 16x16x32 */ \
   X(55, 4, 2, 2, 4, 3, 32, true, 1, true)     /* 256×256, k32 × 3, 16x16x32 */ \
-  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */
+  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */ \
+  /* round 5: 224-row tiles, so the 51200-row GEMMs of C2 (stage 3, the 40² CCFM) fill the 256 CUs in one wave \
+     (229 tiles) instead of 200 256-row tiles; one wave per SIMD, each 224 × 64 */ \
+  X(66, 1, 4, 7, 2, 2, 32, false, 1, false)    /* 224×256, 4 waves of 224×64 */ \
+  X(67, 1, 4, 7, 2, 2, 32, true, 1, false)     /* cfg 66 on 16x16x32 MFMAs */ \
+  X(68, 1, 2, 7, 2, 3, 32, false, 1, false)    /* 224×128, 2 waves of 224×64, k32 × 3 */
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path
