@@ -829,12 +829,11 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(53, 4, 2, 2, 2, 3, 32, true, 1, true)     /* cfg 52 on 16x16x32 MFMAs */ \
   X(54, 4, 2, 2, 2, 4, 32, true, 1, true)     /* 256×128, k32 × 4, 16x16x32 */ \
   X(55, 4, 2, 2, 4, 3, 32, true, 1, true)     /* 256×256, k32 × 3, 16x16x32 */ \
-  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */ \
-  /* round 5: 224-row tiles, so the 51200-row GEMMs of C2 (stage 3, the 40² CCFM) fill the 256 CUs in one wave \
-     (229 tiles) instead of 200 256-row tiles; one wave per SIMD, each 224 × 64 */ \
-  X(66, 1, 4, 7, 2, 2, 32, false, 1, false)    /* 224×256, 4 waves of 224×64 */ \
-  X(67, 1, 4, 7, 2, 2, 32, true, 1, false)     /* cfg 66 on 16x16x32 MFMAs */ \
-  X(68, 1, 2, 7, 2, 3, 32, false, 1, false)    /* 224×128, 2 waves of 224×64, k32 × 3 */
+  X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */
+// (round 5 built 224-row tiles — 224×256 with four waves of 224×64, its 16x16x32 form, 224×128 with two
+// waves — so the 51200-row C2 GEMMs would fill the 256 CUs in one wave of 229 tiles: 1.2-2.3× slower than
+// the table's tiles on all ten 51200-row shapes, profiles/r5/x3/tune_224.json; one wave per SIMD and the
+// A split repeated by every wave cost more than the full wave of CUs gains. Removed.)
 // cfg 46's OCC = 4: registers for 4 waves per SIMD (four workgroups per CU): bit-identical, 1.02-1.09x
 // over the unconstrained allocation (3 per SIMD) on the short-K shapes it serves
 // (profiles/r3/x3/ab_glds_occupancy.jsonl); 122 VGPRs, no spill, on the 1×1 fast path (the general path

@@ -47,7 +47,7 @@ int launch_glds_cfg(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
   // cfg + 100: the slab epilogue (variants 2 / 3); cfg + 200: its direct-store form (variant 4) where it applies
   const int epv = cfg >= 200 ? 4 : cfg >= 100 ? 2 : 1;
   cfg %= 100;
-  if (a.d.A2 || cfg < 11 || cfg > 68) return -2;
+  if (a.d.A2 || cfg < 11 || cfg > 65) return -2;
   return glds_part_k(cfg % kGldsParts, a, planes, cfg, s, epv);
 }
 

@@ -1452,12 +1452,12 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       (cfg == 12 || cfg == 14 || cfg == 41 || cfg == 45 || cfg == 46 || cfg == 47 || cfg == 63 || cfg == 64))
     cfg += g_glds_epv == 4 ? 200 : 100;
   // cfg + 100: the LDS-DMA residual epilogue variant; cfg + 200: its direct-store form
-  const int gc = cfg >= 211 && cfg <= 268 ? cfg - 200 : cfg >= 111 && cfg <= 168 ? cfg - 100 : cfg;
-  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 68)) && !a.d.A2) {
+  const int gc = cfg >= 211 && cfg <= 265 ? cfg - 200 : cfg >= 111 && cfg <= 165 ? cfg - 100 : cfg;
+  if (((gc >= 11 && gc <= 20) || (gc >= 33 && gc <= 38) || (gc >= 41 && gc <= 51) || (gc >= 62 && gc <= 65)) && !a.d.A2) {
     const int rc = launch_glds_cfg(a, planes, cfg, s);
     if (rc != -2) return rc;
   }
-  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 68 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
+  if (cfg < 0 || (cfg > 6 && cfg < 11) || (cfg > 26 && cfg < 31) || (cfg > 38 && cfg < 41) || (cfg > 51 && cfg < 62) || (cfg > 65 && cfg < 70) || (cfg > 75 && gc == cfg) || (cfg >= 73 && cfg <= 75 && (a.splits > 1 || !a.vec_epi)) || (cfg >= 11 && a.d.A2)) {
     // By shape (tools/conv_bench.py sweeps): the LDS-DMA kernel whenever the operands allow it,
     // the largest tile that still gives >= 192 workgroups, a 64-wide N tile for Cout <= 64;
     // 256×256 where Cout is a multiple of 256 and K >= 512 (+10-16 % there; a 384-wide N wastes

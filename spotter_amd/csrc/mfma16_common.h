@@ -92,6 +92,12 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 // v_cvt_pk_bf16_f32, 8 + 8 unpacks (the low half of a pair is `u << 16`, the high half `u &
 // 0xffff0000`: bf16 → fp32 is exact) and 16 v_sub_f32 — 44 instructions, against ~60 for the
 // element-wise form (hipcc converts element by element, then repacks). Same RNE hi / mid / lo as split8.
+// Round 5: the residual subtractions as packed pairs (f32x2 arithmetic → v_pk_add_f32, two lanes of fp32 per
+// instruction): 12 cvt + 16 unpacks + 8 v_pk_add_f32 = 36 VALU per 8 elements. Same values, bit for bit
+// (an fp32 subtraction is exact here either way). -DSP_SPLIT_PK2=0: the scalar-subtraction form (diagnostic A/B).
+#ifndef SP_SPLIT_PK2
+#define SP_SPLIT_PK2 1
+#endif
 template <int PL>
 __device__ __forceinline__ void split_frag_pk(const float4& x0, const float4& x1, bf16x8* out) {
   const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -102,11 +108,22 @@ __device__ __forceinline__ void split_frag_pk(const float4& x0, const float4& x1
     const uint32_t h = cvt_pk_bf16(a, b);
     H[q] = h;
     if constexpr (PL == 3) {
+#if SP_SPLIT_PK2
+      const f32x2 ab = {a, b};
+      const f32x2 hf = {__builtin_bit_cast(float, h << 16), __builtin_bit_cast(float, h & 0xffff0000u)};
+      const f32x2 r = ab - hf;
+      const uint32_t m = cvt_pk_bf16(r.x, r.y);
+      M[q] = m;
+      const f32x2 mf = {__builtin_bit_cast(float, m << 16), __builtin_bit_cast(float, m & 0xffff0000u)};
+      const f32x2 r2 = r - mf;
+      L[q] = cvt_pk_bf16(r2.x, r2.y);
+#else
       const float ra = a - __builtin_bit_cast(float, h << 16);
       const float rb = b - __builtin_bit_cast(float, h & 0xffff0000u);
       const uint32_t m = cvt_pk_bf16(ra, rb);
       M[q] = m;
       L[q] = cvt_pk_bf16(ra - __builtin_bit_cast(float, m << 16), rb - __builtin_bit_cast(float, m & 0xffff0000u));
+#endif
     }
   }
   out[0] = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
