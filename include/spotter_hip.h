@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 12
+#define SP_ABI_VERSION 13
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -107,6 +107,13 @@ typedef struct {
   uint16_t* C_bf16;
   const uint16_t* res1_bf16;
   const uint16_t* res2_bf16;
+  /* ABI v13: split-K arrival counters (optional, with a workspace). When set, a split-K launch combines its
+   * partial sums inside the GEMM launch: each output tile's last-arriving workgroup adds the tile's partials in
+   * fixed split order and applies the epilogue (the same arithmetic as the separate reduce launch, so the
+   * result is bit-identical), instead of a second reduce launch. The caller zeroes the array once before first
+   * use and gives each concurrently running stream its own; every launch leaves it zero. Launches whose tile
+   * grid exceeds splitk_counters_len entries, or tiles without the in-launch form, use the reduce launch. */
+  int32_t* splitk_counters; int64_t splitk_counters_len;
 } sp_conv_desc;
 
 /*

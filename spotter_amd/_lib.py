@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -44,6 +44,7 @@ class SpConvDesc(C.Structure):
         ("ln_gamma", vp), ("ln_beta", vp), ("ln_eps", f32),
         ("A_bf16", vp),
         ("C_bf16", vp), ("res1_bf16", vp), ("res2_bf16", vp),
+        ("splitk_counters", vp), ("splitk_counters_len", i64),
     ]
 
 

@@ -35,6 +35,9 @@ struct ConvArgs {
   // producer instead of rounded per fragment in the GEMM (lda and bs_a count bf16 elements then).
   const uint16_t* A16 = nullptr;
   int64_t a_plane_stride = 0;
+  // split-K with the in-launch combine (splitk_combine): one arrival counter per output tile (set by the
+  // launchers whose kernels call splitk_combine, from sp_conv_desc.splitk_counters); null: the reduce launch
+  int32_t* counters = nullptr;
 };
 
 // Output row offset (elements): plain row-major (out_rows_per_group == 0) or grouped rows.
@@ -137,6 +140,24 @@ __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int
   }
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// A buffer descriptor over the split-K partial slabs (offsets below 2^31 bytes: splitk_counters_for).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t partial_rsrc(const ConvArgs& p) {
+  return __builtin_amdgcn_make_buffer_rsrc(p.partial, 0, 0x7fffffff, 0x00020000);
+}
+
+// One float4 of this workgroup's split-K partial slab (z = blockIdx.z). With the in-launch combine
+// (p.counters) the store is write-through (sc1), so the tile's last workgroup, on any CU or XCD, reads it with
+// sc1 loads and no agent release / acquire fence is needed (cdna_hip_programming.md §6 Guideline 16 R1).
+__device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int n, float4 v) {
+  const int64_t e = ((int64_t)blockIdx.z * p.M + m) * p.ldp + n;
+  if (p.counters)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), partial_rsrc(p), (int)(e * 4), 0, 16);
+  else
+    *reinterpret_cast<float4*>(p.partial + e) = v;
+}
+
 // Accumulator band i of a wave (TN 32x32 MFMA tiles, v_mfma_f32_32x32x*: lane (r, h) holds
 // rows (q&3) + 8(q>>2) + 4h, column r) → the wave's private LDS slab → fused epilogue on
 // float4s of one output row (or raw partial sums for split-K).
@@ -162,7 +183,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
     if (m >= p.M || n >= p.d.Cout) continue;
     float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
     if (p.splits > 1) {
-      *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+      store_partial(p, m, n, v);
     } else {
       epilogue_store<BF>(p, m, n, v);
     }
@@ -225,7 +246,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         if (m >= p.M || n >= d.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
         if (p.splits > 1) {
-          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+          store_partial(p, m, n, v);
         } else if (fastv) {
           epilogue_vec<BF>(p, m, n, v, r1[u]);
         } else {
@@ -233,6 +254,86 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         }
       }
     }
+  }
+}
+
+// The counters a split-K launch of `tiles` output tiles may use: the descriptor's array when it has one
+// entry per tile (and the partial slabs are addressable by 32-bit buffer offsets, at most 16 splits), else
+// null (the separate reduce launch).
+inline int32_t* splitk_counters_for(const ConvArgs& a, int64_t tiles) {
+  return (a.splits > 1 && a.splits <= 16 && a.d.splitk_counters && tiles <= a.d.splitk_counters_len &&
+          (int64_t)a.splits * a.M * a.ldp * 4 < (int64_t(1) << 31))
+             ? a.d.splitk_counters
+             : nullptr;
+}
+
+// In-launch split-K combine (ABI v13), called by every workgroup of a split-K launch with counters after its
+// partial tile went out (store_partial: write-through sc1 stores). The hand-off follows the MI355X guide
+// (cdna_hip_programming.md §5 "In-launch split-K reduction", its sc1 form; §6 Guideline 16 R1): every wave
+// drains its stores, the workgroup meets at a barrier, one lane draws a ticket (relaxed agent-scope add);
+// the workgroup that draws splits − 1 resets the counter for the next launch and combines the tile with sc1
+// loads (no acquire fence): Σ_z partial[z] in z order, then the epilogue — splitk_reduce_kernel's arithmetic,
+// so the output is bit-identical to the two-launch form. Each thread keeps 16 partial loads in flight (its
+// TPT float4 tasks × 16 / TPT splits per round) beside its residual loads. `flag` is a word of the kernel's one LDS array (no second __shared__ object), free
+// once the epilogue is done.
+template <int NT, int BM, int BN>
+__device__ __forceinline__ void splitk_combine(const ConvArgs& p, int* flag, int tile, int64_t m0, int n0) {
+  constexpr int TPT = BM * BN / 4 / NT;  // float4 tasks per thread
+  static_assert(TPT * NT * 4 == BM * BN && TPT <= 16, "combine tasks");
+  constexpr int ZB = 16 / TPT;           // splits loaded per round: TPT · ZB = 16 loads in flight
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through partial stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == p.splits - 1;
+    if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const __amdgpu_buffer_rsrc_t rs = partial_rsrc(p);
+  const int zs = (int)(p.M * p.ldp * 4);  // bytes between split slabs
+  const sp_conv_desc& d = p.d;
+  int64_t mm[TPT];
+  int nn[TPT], off[TPT];
+  bool ok[TPT];
+  float4 v[TPT], r1[TPT];
+#pragma unroll
+  for (int t = 0; t < TPT; ++t) {
+    const int i = threadIdx.x + NT * t;
+    const int row = i / (BN / 4);
+    mm[t] = m0 + row;
+    nn[t] = n0 + (i - row * (BN / 4)) * 4;
+    ok[t] = mm[t] < p.M && nn[t] < d.Cout;
+    off[t] = ok[t] ? (int)((mm[t] * p.ldp + nn[t]) * 4) : 0;
+    // the residual segment in flight with the partials (epilogue_vec's operand)
+    r1[t] = (ok[t] && p.vec_epi && nn[t] + 3 < d.Cout) ? load_res1(d, mm[t], nn[t]) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int z0 = 0; z0 < p.splits; z0 += ZB) {
+    u32x4 u[TPT][ZB];
+#pragma unroll
+    for (int j = 0; j < ZB; ++j)
+      if (z0 + j < p.splits)
+#pragma unroll
+        for (int t = 0; t < TPT; ++t) u[t][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, off[t] + (z0 + j) * zs, 0, 16);
+#pragma unroll
+    for (int j = 0; j < ZB; ++j)
+      if (z0 + j < p.splits)
+#pragma unroll
+        for (int t = 0; t < TPT; ++t) {
+          const float4 w = __builtin_bit_cast(float4, u[t][j]);
+          if (z0 + j == 0) {
+            v[t] = w;
+          } else {
+            v[t].x += w.x; v[t].y += w.y; v[t].z += w.z; v[t].w += w.w;
+          }
+        }
+  }
+#pragma unroll
+  for (int t = 0; t < TPT; ++t) {
+    if (!ok[t]) continue;
+    if (p.vec_epi && nn[t] + 3 < d.Cout) epilogue_vec(p, mm[t], nn[t], v[t], r1[t]);
+    else epilogue_store(p, mm[t], nn[t], v[t]);
   }
 }
 

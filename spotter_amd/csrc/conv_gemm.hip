@@ -242,6 +242,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   for (int i = 0; i < TM; ++i)
     epilogue_band<TN>(p, smem + wave * (32 * TN * 32), acc[i], m0 + wm * TM * 32 + i * 32,
                       n0 + wn * TN * 32, lane);
+  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+    splitk_combine<256, BM, BN>(p, reinterpret_cast<int*>(smem), blockIdx.y * gridDim.x + blockIdx.x, m0, n0);
 }
 
 // Split-K combine: out = epilogue(Σ_z partial[z]) in fixed z order (deterministic).
@@ -264,9 +266,11 @@ template <int TM, int TN, int DB, int WM = 2, bool LN = false>
 int launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * (4 / WM) * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM), a.splits);
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, a);
+  ConvArgs b = a;
+  b.counters = LN ? nullptr : splitk_counters_for(a, (int64_t)grid.x * grid.y);
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, b);
   int rc = check_launch("sp_conv2d");
-  if (rc || a.splits == 1) return rc;
+  if (rc || a.splits == 1 || b.counters) return rc;
   return launch_splitk_reduce(a, s);
 }
 

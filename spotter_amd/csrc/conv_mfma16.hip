@@ -283,6 +283,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
 }
 
 #if SP_X3S_STAMP
@@ -506,6 +508,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
 }
 
 template <int WM, int WN, int TM, int TN, int NS>
@@ -733,6 +737,8 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
   float* smemf = reinterpret_cast<float*>(smem);
   epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
                             lane);
+  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
 }
 
 template <int TM, int TN>
@@ -1028,7 +1034,7 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
         if (m >= p.M || n >= dd.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * W + col);
         if (p.splits > 1) {
-          *reinterpret_cast<float4*>(p.partial + ((int64_t)blockIdx.z * p.M + m) * p.ldp + n) = v;
+          store_partial(p, m, n, v);
         } else if (fastv) {
           epilogue_vec(p, m, n, v, r1[u]);
         } else {
@@ -1348,12 +1354,14 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
     return -1;
   }
   dim3 grid((unsigned)tiles, 1, a.splits);
+  ConvArgs b = a;
+  b.counters = splitk_counters_for(a, tiles);
   if (planes == 3)
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, b);
   else
-    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, a);
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, b);
   int rc = check_launch(planes == 3 ? "sp_conv2d(f32x3)" : "sp_conv2d(bf16)");
-  if (rc || a.splits == 1) return rc;
+  if (rc || a.splits == 1 || b.counters) return rc;
   return launch_splitk_reduce(a, s);
 }
 

@@ -154,7 +154,7 @@ class Engine:
                  fold_repvgg: bool = True, precision: str = "fp32", fuse_shortcut: bool = True,
                  fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4,
                  bf16_store: bool | None = None, direct_c32: bool = True,
-                 direct_c64_bf16: bool = True):
+                 direct_c64_bf16: bool = True, splitk_combine: bool = False):
         from ._lib import lib
 
         if precision not in PRECISIONS:
@@ -205,6 +205,12 @@ class Engine:
         # the fp32-MFMA implicit GEMM
         self.direct_c32 = direct_c32
         self.direct_c64_bf16 = direct_c64_bf16  # the stage-0 3x3 (Cin 64 -> 64) on bf16 rows (sp_conv3x3_c64_bf16)
+        # split-K GEMMs (the small-batch path) combine their partial sums inside the GEMM launch (per-context
+        # arrival counters, sp_conv_desc.splitk_counters) instead of a second reduce launch: bit-identical, 303
+        # instead of 438 launches per bs1 forward, but 4.786 against 4.714 ms per graph replay (the write-through
+        # partial stores and the last workgroup's combine cost more than the reduce launch they replace,
+        # profiles/r5/bs1/bs1_ab_splitk_combine.json), so off by default
+        self.splitk_combine = splitk_combine
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -426,6 +432,20 @@ class Engine:
             ws[key] = t
         return t[:n]
 
+    SPLITK_COUNTERS = 4096  # arrival counters per context: one per output tile of a split-K launch
+
+    def _splitk(self) -> dict:
+        """The split-K scratch of this context's GEMM launches: the partial-sum workspace and, with
+        splitk_combine, the arrival counters (zeroed once here; every launch leaves them zero)."""
+        kw = {"workspace": self._buf("splitk", self.SPLITK_ELEMS)}
+        if self.splitk_combine:
+            c = self._ws.get("splitk_cnt")
+            if c is None:
+                c = torch.zeros(self.SPLITK_COUNTERS, dtype=torch.int32, device=self.dev)
+                self._ws["splitk_cnt"] = c
+            kw["counters"] = c
+        return kw
+
     def _const(self, key, fn):
         c = self._consts.get(key)
         if c is None:
@@ -466,7 +486,7 @@ class Engine:
                               act=act, res1=res1, res2=res2, wino=(cw.wino, work, wm))
         return ops.conv2d(x, n, h, w, cw.cin, cw.w, cw.cout, cw.k, stride, pad, out, scale=cw.scale,
                           shift=cw.shift, act=act, res1=res1, res2=res2,
-                          workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(cw.w16), **kw)
+                          **self._splitk(), **_wkw(cw.w16), **kw)
 
     def _lin_op(self, x: V, rows, lw: LinW, out: V, act=None, res1=None, res2=None, a2=None, row_scale=None,
                 ln=None):
@@ -485,10 +505,10 @@ class Engine:
         if ln is not None:  # unfused: GEMM into a scratch row block, then sp_layernorm into `out`
             tmp = view(self._buf("ln_tmp", rows, lw.n), lw.n)
             ops.linear(x, rows, lw.k, lw.w, lw.n, tmp, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                       row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
+                       row_scale=row_scale, **self._splitk(), **_wkw(lw.w16))
             return ops.layernorm(tmp, *ln, out, rows, lw.n, self.cfg.layer_norm_eps)
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                          row_scale=row_scale, workspace=self._buf("splitk", self.SPLITK_ELEMS), **_wkw(lw.w16))
+                          row_scale=row_scale, **self._splitk(), **_wkw(lw.w16))
 
     C64_MIN_PIXELS = 1 << 18
     C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)

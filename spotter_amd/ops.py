@@ -78,12 +78,15 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
            pad: int, out: V, *, scale=None, shift=None, act=None, res1: V | None = None,
            res2: V | None = None, a2: V | None = None, row_scale: torch.Tensor | None = None,
            rows_per_group: int = 0, group_stride: int = 0, workspace: torch.Tensor | None = None,
-           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None):
+           wt16: torch.Tensor | None = None, wt_planes: torch.Tensor | None = None, ln=None, wino=None,
+           counters: torch.Tensor | None = None):
     """ln = (gamma, beta, eps): LayerNorm over each output row fused into the epilogue (fp32 weights).
     wino = (planes, work[, m]): run this 3×3 stride-1 conv as Winograd F(m×m, 3×3), m = 2 (default) or 4
     (sp_winograd_f23_* / _f43_*), on the transformed weight planes (int16 [3 or 1, (m+2)²·Cout·Cin],
     winograd_weights_host + split) with the fp32 scratch `work`; the bf16 / split operand mode follows the
     plane count.
+    counters (int32, zeroed once by the caller, one per stream): split-K launches combine their partial sums
+    inside the GEMM launch (sp_conv_desc.splitk_counters, ABI v13) instead of a second reduce launch.
     wt16 (int16 bit patterns of bf16 weights, same [Cout][K] layout) selects the bf16 MFMA path;
     wt_planes (int16 [3, Cout*K]: the hi / mid / lo bf16 split of the fp32 weights, split_bf16x3)
     selects the fp32-accurate 3-way-split path (SP_PREC_F32X3)."""
@@ -168,6 +171,11 @@ def conv2d(x: V, n: int, h: int, w: int, cin: int, wt: torch.Tensor, cout: int, 
         assert workspace.dtype == torch.float32 and workspace.is_cuda
         d.workspace = workspace.data_ptr()
         d.workspace_elems = workspace.numel()
+    if counters is not None:
+        if counters.dtype != torch.int32 or not counters.is_cuda or not counters.is_contiguous():
+            raise ValueError("conv: split-K counters must be a contiguous int32 CUDA tensor")
+        d.splitk_counters = counters.data_ptr()
+        d.splitk_counters_len = counters.numel()
     # compulsory bytes: activations at their storage width (fp32 or bf16 rows), weights in the operand form
     # the GEMM streams (fp32, one bf16 plane, or the three split planes)
     wbytes = 2 if wt16 is not None else 6 if wt_planes is not None else 4
@@ -217,10 +225,10 @@ def wino_work_elems(wm: int, tiles: int, cin: int, cout: int) -> int:
 
 def linear(x: V, rows: int, k: int, wt: torch.Tensor, n: int, out: V, *, bias=None, act=None,
            res1: V | None = None, res2: V | None = None, a2: V | None = None, row_scale=None,
-           scale=None, workspace=None, wt16=None, wt_planes=None, ln=None):
+           scale=None, workspace=None, wt16=None, wt_planes=None, ln=None, counters=None):
     return conv2d(x, 1, 1, rows, k, wt, n, 1, 1, 0, out, scale=scale, shift=bias, act=act, res1=res1,
                   res2=res2, a2=a2, row_scale=row_scale, workspace=workspace, wt16=wt16, wt_planes=wt_planes,
-                  ln=ln)
+                  ln=ln, counters=counters)
 
 
 def bf16_bits(a) -> np.ndarray:

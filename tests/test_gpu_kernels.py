@@ -167,6 +167,48 @@ def test_splitk_tiles_bit_identical(dev, mode, cfg):
         assert np.array_equal(outs[1], outs[0]), (case, mode, cfg)
 
 
+@pytest.mark.parametrize("mode", ["f32", "x3", "bf16"])
+def test_splitk_in_launch_combine_bit_identical(dev, mode):
+    """Split-K with arrival counters (ABI v13 sp_conv_desc.splitk_counters: the tile's last-arriving
+    workgroup sums the partials in z order and applies the epilogue inside the GEMM launch) gives the bits of
+    the two-launch form (partials, then splitk_reduce_kernel), on the fp32-MFMA and the register-staged split /
+    bf16 tiles, with BN, residuals before and after the activation and a ragged Cout. Three launches in a row
+    each leave every counter at zero, and a counter array shorter than the tile grid falls back to the reduce
+    launch."""
+    from spotter_amd import ops
+    from spotter_amd.ops import view
+
+    ws = torch.empty(4 << 20, device=dev)
+    cnt = torch.zeros(4096, dtype=torch.int32, device=dev)
+    for case in SPLITK_CASES + [(1, 12, 12, 512, 202, 3, 1, "relu")]:
+        n, h, w, cin, cout, k, st, act = case
+        rng = np.random.default_rng(seed(case) + 1)
+        x = T(rng.standard_normal((n * h * w * cin,)).astype(np.float32), dev)
+        wt = T((rng.standard_normal((cout, k * k * cin)) / np.sqrt(cin * k * k)).astype(np.float32), dev)
+        pad = k // 2
+        ho, wo = (h + 2 * pad - k) // st + 1, (w + 2 * pad - k) // st + 1
+        m = n * ho * wo
+        r1 = view(T(rng.standard_normal(m * cout).astype(np.float32), dev), cout)
+        r2 = view(T(rng.standard_normal(m * cout).astype(np.float32), dev), cout)
+        sc = T(rng.uniform(0.5, 1.5, cout).astype(np.float32), dev)
+        sh = T(rng.standard_normal(cout).astype(np.float32), dev)
+        kw = {"f32": {}, "x3": {"wt_planes": ops.split_bf16x3(wt)},
+              "bf16": {"wt16": T(ops.bf16_bits(wt.cpu().numpy()).view(np.int16), dev)}}[mode]
+
+        def run(counters):
+            out = torch.full((m * cout,), float("nan"), device=dev)
+            ops.conv2d(view(x, cin), n, h, w, cin, wt, cout, k, st, pad, view(out, cout), scale=sc, shift=sh,
+                       act=act, res1=r1, res2=r2, workspace=ws, counters=counters, **kw)
+            return out.cpu().numpy()
+
+        ref = run(None)
+        assert not np.isnan(ref).any()
+        for _ in range(3):
+            assert np.array_equal(run(cnt), ref), (case, mode)
+            assert int(cnt.abs().sum()) == 0, (case, mode)
+        assert np.array_equal(run(cnt[:1]), ref), (case, mode)
+
+
 def _bf16(a):
     u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
     return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)

@@ -54,6 +54,35 @@ def test_library_exports_every_header_symbol():
     assert L.sp_abi_version() == _lib.ABI_VERSION
 
 
+def test_ctypes_descriptors_match_the_header_layout(tmp_path):
+    """The ctypes mirrors of the C-ABI descriptor structs (spotter_amd/_lib.py) have the header's size and
+    field offsets, checked against a C program compiled from include/spotter_hip.h."""
+    import ctypes
+
+    from spotter_amd import _lib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    structs = {"sp_conv_desc": _lib.SpConvDesc, "sp_msda_desc": _lib.SpMsdaDesc}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "spotter_hip.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        cname, f, v = ln.split()
+        got[(cname, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
 def test_product_library_reads_no_environment():
     """Tile / transform choices come from the ABI (sp_set_conv_config) and the compiled tables only: the
     environment overrides of the tuning tools exist only in an SP_TUNING_BUILD=1 library."""

@@ -24,6 +24,10 @@ import torch  # noqa: E402
 from tune_conv import F32_CFGS, time_one  # noqa: E402
 
 X3_CANDIDATES = ["-", "12", "14", "33", "41", "44", "47", "63", "214", "245", "246", "247", "263", "212", "241"]
+# bf16 rows: the slab-epilogue tiles (cfg, launched as cfg + 100) and the transposed-roles register epilogue
+# (cfg + 300, 32x32 blocks only)
+BF16_CANDIDATES = ["-", "12", "13", "14", "16", "33", "41", "45", "47", "52", "53", "63", "64",
+                   "312", "313", "314", "316", "333", "345", "352", "363", "364"]
 
 
 def main():
@@ -34,6 +38,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--min-ms", type=float, default=0.1, help="shapes cheaper than this per step are skipped")
     ap.add_argument("--modes", default="x3,f32")
+    ap.add_argument("--cands", default="", help="comma-separated candidate list (default: by mode)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -47,7 +52,8 @@ def main():
             continue
         rows = "rows" in key[6:]
         epi = next((t[4:] for t in key[6:] if isinstance(t, str) and t.startswith("epi:")), "none")
-        cands = F32_CFGS if mode == "f32" else X3_CANDIDATES
+        cands = (a.cands.split(",") if a.cands else
+                 F32_CFGS if mode == "f32" else BF16_CANDIDATES if mode == "bf16" else X3_CANDIDATES)
         rounds = {c: [] for c in cands}
         for _ in range(a.rounds):
             for c in cands:
