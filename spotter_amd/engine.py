@@ -250,7 +250,7 @@ class Engine:
         (self.winograd) selects."""
         if cw.k != 3 or cw.mode == "f32" or cw.cin % 32 or cw.cout % 4 or not self.winograd:
             return cw
-        if self.winograd == "auto" and (cw.cin < (128 if self.wino_m == 4 else 256) or cw.mode != "x3"):
+        if self.winograd == "auto" and (cw.cin < (self.WINO43_MIN_CIN if self.wino_m == 4 else 256) or cw.mode != "x3"):
             return cw
         u = ops.winograd_weights_host(cw.host.reshape(cw.cout, 3, 3, cw.cin), self.wino_m)
         if cw.mode == "x3":
@@ -455,6 +455,10 @@ class Engine:
 
     # ------------------------------------------------------------------ layers
     SPLITK_ELEMS = 16 << 20  # 64 MB fp32 split-K scratch per context
+    # F(4x4) Winograd from Cin 128. Round 5 measured Cin 64 (the stage-1 160²×64 3x3s): 0.50 against 0.65 ms
+    # for the implicit GEMM in isolation (profiles/r5/wino/tune_wino_c64.json), but no change in the C2 step
+    # (772-774 img/s either way, same box, alternating) and 0.2 % slower at bs1 (profiles/r5/wino/ab_cin64.json)
+    WINO43_MIN_CIN = 128
     WINO_MIN_PIXELS = 8192
     WINO43_MIN_WORK = 1 << 19
 
@@ -465,7 +469,7 @@ class Engine:
         40²x384 / 80²x128 convs measured 2.6x / 1.45x / 1.09x, 40²x256 1.04x, 20²x384 / 20²x512 0.85-0.95x
         (profiles/r2/tune_wino_f43_bs1.json); every bs8 / bs32 map clears it."""
         if self.wino_m == 4:
-            return pixels * cin >= self.WINO43_MIN_WORK
+            return pixels * cin >= self.WINO43_MIN_WORK and cin >= self.WINO43_MIN_CIN
         return pixels >= self.WINO_MIN_PIXELS
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):

@@ -1,7 +1,7 @@
 """bs1 forward A/B on hipGraph replays: the split-K launches' tile, split cap and minimum k-tiles
-(sp_set_splitk_config), the split-K combine (in the GEMM launch, or "sep": the separate reduce launch,
-Engine.splitk_combine) and the fused post-LayerNorm epilogue (Engine.fuse_ln, diagnostic builds), same
-process, variants interleaved over several rounds.
+(sp_set_splitk_config), the split-K combine ("comb": inside the GEMM launch, Engine.splitk_combine; else
+the reduce launch) and the fused post-LayerNorm epilogue (Engine.fuse_ln, diagnostic builds), same process,
+variants interleaved over several rounds.
 
     python tools/bs1_ab.py [--preset r101vd] [--reps 100] [--rounds 3] [--variants plain:-1:16:8,ln:-1,...]
 
@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="plain:-1:16:8,sep:-1:16:8,plain:-1:16:4,plain:-1:8:8")
+    ap.add_argument("--variants", default="plain:-1:16:8,comb:-1:16:8")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     cfg = PRESETS[a.preset]
@@ -36,13 +36,13 @@ def main():
     eng = Engine(cfg, generate(cfg, seed=0), dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
-    dflt = ["plain", "-1", "16", "8"]  # plain|sep|ln : split-K tile : max splits : min k-tiles
+    dflt = ["plain", "-1", "16", "8"]  # plain|comb|ln : split-K tile : max splits : min k-tiles
     variants = [(lambda q: q + dflt[len(q):])(v.split(":")) for v in a.variants.split(",")]
     runners, ref = {}, None
     res = {}
     for mode, c, ms, mk in variants:
         eng.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
-        eng.splitk_combine = mode != "sep"  # "sep": split-K partials reduced by a second launch
+        eng.splitk_combine = mode == "comb"  # "comb": split-K combined inside the GEMM launch
         ops.force_splitk_config(c, int(ms), int(mk))
         try:
             r = GraphRunner(eng, 1, cfg.image_size, cfg.image_size)
