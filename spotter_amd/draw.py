@@ -12,15 +12,18 @@ here is Pillow's ImageDraw with its default font replaced by the same font whose
 
 Exactness: a key is served from the memo only after two renders at *different* start fractions of its class
 gave identical masks (a key whose masks differ is never memoised again); fractions within 1e-5 of a class
-boundary, negative fractions and every non-default option are rendered by Pillow as before. The masks are
-pure functions of those inputs, and draw_bitmap then composites them exactly as Pillow does, so the drawn
-pixels are Pillow's (tests/test_draw.py: all amenity strings over dense start grids; the whole serve.py tail
+boundary, negative fractions and every non-default option are rendered by Pillow as before. A render at
+exactly the same start (string, options and both start coordinates equal) is also served again from a bounded
+cache (`EXACT_CAP` entries, least recently used out): the same inputs, so the same mask. The masks are pure
+functions of those inputs, and draw_bitmap then composites them exactly as Pillow does, so the drawn pixels
+are Pillow's (tests/test_draw.py: all amenity strings over dense start grids; the whole serve.py tail
 byte-identical on the GPU box).
 """
 from __future__ import annotations
 
 import threading
 import types
+from collections import OrderedDict
 
 from PIL import ImageDraw as _PILDraw
 from PIL import ImageFont as _PILFont
@@ -44,32 +47,56 @@ def start_class(f: float, upper: float):
 class _MemoFont(_PILFont.FreeTypeFont):
     """Pillow's default FreeType font (ImageFont.load_default()) with memoised getmask2."""
 
+    EXACT_CAP = 4096  # renders kept for an exact repeat of (string, options, start)
+
     def _memo_init(self):
         self._memo_lock = threading.Lock()
         self._memo: dict = {}        # key -> (mask, offset) once verified
         self._pending: dict = {}     # key -> (start pair, mask signature) of its first render
         self._no_memo: set = set()
-        self.memo_stats = {"hits": 0, "renders": 0, "bypass": 0}
+        self._exact: OrderedDict = OrderedDict()  # (string, options, exact start) -> (mask, offset)
+        self.memo_stats = {"hits": 0, "exact_hits": 0, "renders": 0, "bypass": 0}
+
+    def _exact_put(self, ekey, val):
+        with self._memo_lock:
+            self._exact[ekey] = val
+            if len(self._exact) > self.EXACT_CAP:
+                self._exact.popitem(last=False)
 
     def getmask2(self, text, mode="", *args, start=None, **kwargs):
-        key = None
+        key = ekey = None
         if not args and isinstance(text, str) and start is not None:
-            cx, cy = start_class(float(start[0]), _UPPER_X), start_class(float(start[1]), _UPPER_Y)
-            if cx is not None and cy is not None:
-                try:
-                    key = (text, mode, cx, cy, tuple(sorted(
-                        (k, tuple(v) if isinstance(v, list) else v) for k, v in kwargs.items())))
-                    hash(key)
-                except TypeError:
-                    key = None
+            try:
+                opts = tuple(sorted((k, tuple(v) if isinstance(v, list) else v) for k, v in kwargs.items()))
+                sx, sy = float(start[0]), float(start[1])
+                ekey = (text, mode, sx, sy, opts)
+                hash(ekey)
+            except (TypeError, ValueError, IndexError):
+                ekey = None
+            if ekey is not None:
+                cx, cy = start_class(sx, _UPPER_X), start_class(sy, _UPPER_Y)
+                if cx is not None and cy is not None:
+                    key = (text, mode, cx, cy, opts)
+        if ekey is not None:
+            with self._memo_lock:
+                hit = self._exact.get(ekey)
+                if hit is not None:
+                    self._exact.move_to_end(ekey)
+            if hit is not None:
+                self.memo_stats["exact_hits"] += 1
+                return hit
         if key is None or key in self._no_memo:
             self.memo_stats["bypass"] += 1
-            return super().getmask2(text, mode, *args, start=start, **kwargs)
+            out = super().getmask2(text, mode, *args, start=start, **kwargs)
+            if ekey is not None:
+                self._exact_put(ekey, out)
+            return out
         hit = self._memo.get(key)
         if hit is not None:
             self.memo_stats["hits"] += 1
             return hit
         mask, offset = super().getmask2(text, mode, start=start, **kwargs)
+        self._exact_put(ekey, (mask, offset))
         self.memo_stats["renders"] += 1
         sig = (bytes(mask), mask.size, tuple(offset))
         with self._memo_lock:

@@ -332,15 +332,20 @@ class DeviceRGBImage(_PILImage.Image):
         if info:
             self.info = dict(info)
         if host is None:
+            # the host copy as RGBX rows (X = 255): Pillow's own 4-byte pixel layout, which load() unpacks with a
+            # straight 4-byte copy (0.48 against 0.98 ms for packed RGB through a bytes object on the CPU here)
             dev = rgb_dev.device
-            host = torch.empty(rgb_dev.shape, dtype=torch.uint8, pin_memory=True)
+            host = torch.empty((H, W, 4), dtype=torch.uint8, pin_memory=True)
             side = _side_stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):
-                host.copy_(rgb_dev, non_blocking=True)
+                x4 = torch.full((H, W, 4), 255, dtype=torch.uint8, device=dev)
+                x4[..., :3].copy_(rgb_dev)
+                host.copy_(x4, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(side)
             rgb_dev.record_stream(side)
+            x4.record_stream(side)
         self._pending = (host, done)
 
     def _lazy_copy(self):
@@ -350,7 +355,7 @@ class DeviceRGBImage(_PILImage.Image):
         if self._im is None and getattr(self, "_pending", None) is not None:
             host, done = self._pending
             done.synchronize()
-            self.im = _PILImage.frombytes("RGB", self._size, host.numpy().tobytes()).im
+            self.im = _PILImage.frombytes("RGB", self._size, memoryview(host.numpy()).cast("B"), "raw", "RGBX").im
         return super().load()
 
     def convert(self, mode=None, *args, **kwargs):

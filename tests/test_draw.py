@@ -75,3 +75,25 @@ def test_draw_module_is_pillows_otherwise():
     d2.text((1, 1), "x", font=own)
     with pytest.raises(TypeError):
         shim.Draw()
+
+
+def test_exact_repeats_are_cached_and_bounded():
+    """A render at exactly the same (string, options, start) is served again from the bounded exact cache, also
+    for starts the class memo does not use (a fraction next to a class boundary); the cache keeps at most
+    EXACT_CAP entries."""
+    from spotter_amd.draw import _UPPER_X, _MemoFont
+
+    f = ImageFont.load_default()
+    f.__class__ = _MemoFont
+    f._memo_init()
+    f.EXACT_CAP = 8
+    fresh = ImageFont.load_default()
+    kw = dict(direction=None, features=None, language=None, stroke_width=1, stroke_filled=True, anchor="la", ink=0)
+    for start in ((3.25, 7.5), (2.0 + _UPPER_X, 1e-9)):  # a class-memo key, then a bypassed start
+        a = f.getmask2("sofa", "L", start=start, **kw)
+        b = f.getmask2("sofa", "L", start=start, **kw)
+        assert b is a and _sig(a) == _sig(fresh.getmask2("sofa", "L", start=start, **kw))
+    assert f.memo_stats["exact_hits"] == 2
+    for i in range(20):  # distinct strings: no class-memo hits, every render enters the exact cache
+        f.getmask2(f"bed {i}", "L", start=(0.3, 0.3), **kw)
+    assert len(f._exact) == 8 and ("bed 19", "L", 0.3, 0.3) == next(reversed(f._exact))[:4]

@@ -80,8 +80,10 @@ def opener(decode: str):
     return (lambda data: Image.open(io.BytesIO(data))), ImageDraw
 
 
-async def process_image(client, url, proc, model, stamps, open_fn=None):
-    """One image of a /detect request (serve.py:79-148 order), with per-stage time stamps."""
+async def process_image(client, url, proc, model, stamps, open_fn=None, jitter=None):
+    """One image of a /detect request (serve.py:79-148 order), with per-stage time stamps. jitter (a numpy
+    Generator): shift every box by one random sub-pixel offset per image before drawing, so a benchmark that
+    repeats one image draws at varied fractional positions like varied traffic does."""
     import torch
 
     open_fn, ImageDraw = open_fn or opener("gpu")
@@ -99,6 +101,9 @@ async def process_image(client, url, proc, model, stamps, open_fn=None):
                                                  threshold=0.5)[0]
         labels = [model.config.id2label[int(l.item())] for l in det["labels"]]
         boxes = det["boxes"].tolist()
+        if jitter is not None:
+            dx, dy = (float(v) for v in jitter.random(2))
+            boxes = [[b[0] + dx, b[1] + dy, b[2] + dx, b[3] + dy] for b in boxes]
         t3 = time.perf_counter()
         draw = ImageDraw.Draw(image)
         found = []
@@ -121,7 +126,7 @@ async def process_image(client, url, proc, model, stamps, open_fn=None):
     return {"url": url, "detections": found, "labeled_image_base64": b64}
 
 
-async def handle(body: bytes, client, proc, model, stamps, open_fn=None):
+async def handle(body: bytes, client, proc, model, stamps, open_fn=None, jitter=None):
     """serve.py:179-196: parse the request, process its images, build the response JSON."""
     from pydantic import BaseModel, HttpUrl
 
@@ -129,14 +134,14 @@ async def handle(body: bytes, client, proc, model, stamps, open_fn=None):
         image_urls: list[HttpUrl]
 
     req = DetectionRequest.model_validate(json.loads(body))
-    results = await asyncio.gather(*[process_image(client, str(u), proc, model, stamps, open_fn)
+    results = await asyncio.gather(*[process_image(client, str(u), proc, model, stamps, open_fn, jitter)
                                      for u in req.image_urls])
     found = sorted({d["label"] for r in results for d in r["detections"]})
     desc = f"The property contains: {', '.join(found)}." if found else "No relevant amenities detected."
     return json.dumps({"amenities_description": desc, "images": results})
 
 
-def measure(preset="r101vd", iters=200, model=None, decode="gpu"):
+def measure(preset="r101vd", iters=200, model=None, decode="gpu", jitter=False):
     import httpx
     import numpy as np
     import torch
@@ -151,13 +156,14 @@ def measure(preset="r101vd", iters=200, model=None, decode="gpu"):
     proc = SpotterImageProcessor()
     body = json.dumps({"image_urls": [url]}).encode()
     open_fn = opener(decode)
+    rng = np.random.default_rng(0) if jitter else None
 
     async def run():
         stamps, total = {}, []
         async with httpx.AsyncClient() as client:
             for i in range(iters + 5):
                 t0 = time.perf_counter()
-                await handle(body, client, proc, model, stamps if i >= 5 else {}, open_fn)
+                await handle(body, client, proc, model, stamps if i >= 5 else {}, open_fn, rng)
                 if i >= 5:
                     total.append((time.perf_counter() - t0) * 1e3)
         return stamps, total
@@ -172,7 +178,7 @@ def measure(preset="r101vd", iters=200, model=None, decode="gpu"):
                       "preprocess, forward, post-process, labels, draw, JPEG re-encode, base64, response JSON), "
                       "bs1, 1200x717 JPEG",
             "p50_ms": round(float(np.percentile(total, 50)), 3), "p95_ms": round(float(np.percentile(total, 95)), 3),
-            "iters": iters, "preset": preset, "decode": decode,
+            "iters": iters, "preset": preset, "decode": decode, "box_jitter": bool(jitter),
             "stages_p50_ms": {k: round(float(np.percentile(v, 50)), 3) for k, v in stamps.items()}}
 
 
@@ -181,8 +187,9 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--preset", default="r101vd")
     ap.add_argument("--decode", default="gpu", choices=["gpu", "host"])
+    ap.add_argument("--jitter", action="store_true", help="draw each request's boxes at a random sub-pixel offset")
     a = ap.parse_args()
-    print(json.dumps(measure(a.preset, a.iters, decode=a.decode)))
+    print(json.dumps(measure(a.preset, a.iters, decode=a.decode, jitter=a.jitter)))
 
 
 if __name__ == "__main__":
