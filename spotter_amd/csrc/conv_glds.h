@@ -830,6 +830,9 @@ int launch_glds(const ConvArgs& a, int planes, hipStream_t s, int epv = 1) {
   X(54, 4, 2, 2, 2, 4, 32, true, 1, true)     /* 256×128, k32 × 4, 16x16x32 */ \
   X(55, 4, 2, 2, 4, 3, 32, true, 1, true)     /* 256×256, k32 × 3, 16x16x32 */ \
   X(56, 2, 2, 2, 2, 4, 32, true, 1, true)     /* 128×128, k32 × 4, 16x16x32 */
+// (round 5 also built 256×256 bf16-row tiles with 4 and 5 stages of 32 KB at one workgroup per CU, for the
+// long-K 3x3s: 1.1-2.3× slower than the table's tiles on all 35 C3 / C2-bf16 shapes above 0.3 ms per step,
+// 0.71 against 0.61 ms even at 102400×512×4608, profiles/r5/bf16/retune_*_256x256.json. Removed.)
 // (round 5 built 224-row tiles — 224×256 with four waves of 224×64, its 16x16x32 form, 224×128 with two
 // waves — so the 51200-row C2 GEMMs would fill the 256 CUs in one wave of 229 tiles: 1.2-2.3× slower than
 // the table's tiles on all ten 51200-row shapes, profiles/r5/x3/tune_224.json; one wave per SIMD and the

@@ -57,7 +57,7 @@ def main():
                 continue
             times = {c: t for c, t in e["times"].items() if ":" not in c}
             if not e.get("rows", False):  # fp32-A launches: the bf16-row-only tiles are not theirs
-                times = {c: t for c, t in times.items() if c == "-" or not 52 <= int(c) <= 56}
+                times = {c: t for c, t in times.items() if c == "-" or not 52 <= int(c) % 100 <= 59}
             d = times.get("-")
             best = min(times, key=times.get) if times else "-"
             if d is None or best == "-" or times[best] > d * (1 - a.min_gain):
