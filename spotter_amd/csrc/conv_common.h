@@ -150,9 +150,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t partial_rsrc(const ConvArgs& p
 // One float4 of this workgroup's split-K partial slab (z = blockIdx.z). With the in-launch combine
 // (p.counters) the store is write-through (sc1), so the tile's last workgroup, on any CU or XCD, reads it with
 // sc1 loads and no agent release / acquire fence is needed (cdna_hip_programming.md §6 Guideline 16 R1).
+// CNT: compiled only into the kernels that take counters (conv_mfma16_kernel, conv_gemm_kernel); every other
+// kernel keeps the plain store and never reads p.counters (no extra SGPRs in their epilogues).
+template <bool CNT = false>
 __device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int n, float4 v) {
   const int64_t e = ((int64_t)blockIdx.z * p.M + m) * p.ldp + n;
-  if (p.counters)
+  if (CNT && p.counters)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), partial_rsrc(p), (int)(e * 4), 0, 16);
   else
     *reinterpret_cast<float4*>(p.partial + e) = v;
@@ -161,7 +164,7 @@ __device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int 
 // Accumulator band i of a wave (TN 32x32 MFMA tiles, v_mfma_f32_32x32x*: lane (r, h) holds
 // rows (q&3) + 8(q>>2) + 4h, column r) → the wave's private LDS slab → fused epilogue on
 // float4s of one output row (or raw partial sums for split-K).
-template <int TN, bool BF = false>
+template <int TN, bool BF = false, bool CNT = false>
 __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, const f32x16* accrow,
                                               int64_t mb, int nb, int lane) {
   constexpr int WN = TN * 32;
@@ -183,7 +186,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
     if (m >= p.M || n >= p.d.Cout) continue;
     float4 v = *reinterpret_cast<const float4*>(slab + row * WN + col);
     if (p.splits > 1) {
-      store_partial(p, m, n, v);
+      store_partial<CNT>(p, m, n, v);
     } else {
       epilogue_store<BF>(p, m, n, v);
     }
@@ -197,7 +200,7 @@ __device__ __forceinline__ void epilogue_band(const ConvArgs& p, float* slab, co
 // region fits in the operand stages' LDS, else 1 (band by band).
 // L16: the f32x16 of each 32×32 block holds 2×2 blocks of v_mfma_f32_16x16x32 results (element
 // q = 8·bi + 4·bj + reg; lane l holds rows 16bi + 4(l >> 4) + reg, column 16bj + (l & 15)).
-template <int TM, int TN, int NB, bool L16 = false, bool BF = false>
+template <int TM, int TN, int NB, bool L16 = false, bool BF = false, bool CNT = false>
 __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, f32x16 (*acc)[TN],
                                               int64_t mb, int nb, int lane) {
   static_assert(TM % NB == 0, "bands per round must divide TM");
@@ -246,7 +249,7 @@ __device__ __forceinline__ void epilogue_tile(const ConvArgs& p, float* region, 
         if (m >= p.M || n >= d.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * WN + col);
         if (p.splits > 1) {
-          store_partial(p, m, n, v);
+          store_partial<CNT>(p, m, n, v);
         } else if (fastv) {
           epilogue_vec<BF>(p, m, n, v, r1[u]);
         } else {

@@ -44,7 +44,9 @@ __device__ __forceinline__ int swz(int row, int chunk) { return row * BK + ((chu
 
 // WM × WN waves (WM·WN = 4), each a (32·TM) × (32·TN) patch: 2×2 is the square default, 4×1 gives
 // the 32- and 64-wide N tiles that thin outputs (Cout = 32 / 64: stem, stage 1) need without idle MFMAs.
-template <int TM, int TN, int DB, int WM = 2, bool LN = false>
+// CNT: the split-K launches, which may combine in the launch (splitk_combine); every other instance keeps the
+// plain epilogue.
+template <int TM, int TN, int DB, int WM = 2, bool LN = false, bool CNT = false>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   constexpr int WN = 4 / WM;
   static_assert(WM * WN == 4, "four waves per workgroup");
@@ -240,10 +242,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
-    epilogue_band<TN>(p, smem + wave * (32 * TN * 32), acc[i], m0 + wm * TM * 32 + i * 32,
-                      n0 + wn * TN * 32, lane);
-  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
-    splitk_combine<256, BM, BN>(p, reinterpret_cast<int*>(smem), blockIdx.y * gridDim.x + blockIdx.x, m0, n0);
+    epilogue_band<TN, false, CNT>(p, smem + wave * (32 * TN * 32), acc[i], m0 + wm * TM * 32 + i * 32,
+                                  n0 + wn * TN * 32, lane);
+  if constexpr (CNT) {
+    if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+      splitk_combine<256, BM, BN>(p, reinterpret_cast<int*>(smem), blockIdx.y * gridDim.x + blockIdx.x, m0, n0);
+  }
 }
 
 // Split-K combine: out = epilogue(Σ_z partial[z]) in fixed z order (deterministic).
@@ -262,13 +266,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
   }
 }
 
-template <int TM, int TN, int DB, int WM = 2, bool LN = false>
+template <int TM, int TN, int DB, int WM = 2, bool LN = false, bool CNT = false>
 int launch(const ConvArgs& a, hipStream_t s) {
   constexpr int BM = 32 * WM * TM, BN = 32 * (4 / WM) * TN;
   dim3 grid((a.d.Cout + BN - 1) / BN, (unsigned)((a.M + BM - 1) / BM), a.splits);
   ConvArgs b = a;
-  b.counters = LN ? nullptr : splitk_counters_for(a, (int64_t)grid.x * grid.y);
-  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN>), grid, dim3(256), 0, s, b);
+  b.counters = CNT ? splitk_counters_for(a, (int64_t)grid.x * grid.y) : nullptr;
+  hipLaunchKernelGGL((conv_gemm_kernel<TM, TN, DB, WM, LN, CNT>), grid, dim3(256), 0, s, b);
   int rc = check_launch("sp_conv2d");
   if (rc || a.splits == 1 || b.counters) return rc;
   return launch_splitk_reduce(a, s);
@@ -421,7 +425,7 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     cfg = tile_table_lookup(a.M, d->Cout, a.K, d->KH, d->stride, planes);
   if (cfg < 0 && a.splits > 1 && planes && g_forced_splitk_cfg >= 0) cfg = g_forced_splitk_cfg;
   if (planes) return launch_mfma16(a, planes, cfg, s);
-  if (a.splits > 1) return launch<1, 1, 0>(a, s);
+  if (a.splits > 1) return launch<1, 1, 0, 2, false, true>(a, s);
   switch (cfg) {
     case 220: return launch<2, 2, 0>(a, s);
     case 221: return launch<2, 2, 1>(a, s);

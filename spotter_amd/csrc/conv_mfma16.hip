@@ -53,7 +53,9 @@ namespace sp {
 
 namespace {
 
-template <int WM, int WN, int TM, int TN, int PL, bool FAST>
+// CNT: a split-K instance, which may combine in the launch (splitk_combine); other instances keep the plain
+// epilogue.
+template <int WM, int WN, int TM, int TN, int PL, bool FAST, bool CNT = false>
 __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArgs p) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 32 * TM * WM;
@@ -281,10 +283,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_mfma16_kernel(const ConvArg
   }
 
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
-                            lane);
-  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
-    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  epilogue_tile<TM, TN, NB, false, PL == 1, CNT>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
+                                                  n0 + wn * TN * 32, lane);
+  if constexpr (CNT) {
+    if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+      splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  }
 }
 
 #if SP_X3S_STAMP
@@ -506,10 +510,12 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_pipe_kernel(const ConvArgs 
 
   __syncthreads();
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
-                            lane);
-  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
-    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  epilogue_tile<TM, TN, NB, false, PL == 1, CNT>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
+                                                  n0 + wn * TN * 32, lane);
+  if constexpr (CNT) {
+    if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+      splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  }
 }
 
 template <int WM, int WN, int TM, int TN, int NS>
@@ -735,10 +741,12 @@ __global__ __launch_bounds__(512) void conv_pp_kernel(const ConvArgs p) {
 
   __syncthreads();
   float* smemf = reinterpret_cast<float*>(smem);
-  epilogue_tile<TM, TN, NB, false, PL == 1>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32, n0 + wn * TN * 32,
-                            lane);
-  if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
-    splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  epilogue_tile<TM, TN, NB, false, PL == 1, CNT>(p, smemf + wave * (NB * 32 * TN * 32), acc, m0 + wm * TM * 32,
+                                                  n0 + wn * TN * 32, lane);
+  if constexpr (CNT) {
+    if (p.counters)  // split-K, combined in this launch by the tile's last workgroup
+      splitk_combine<NT, BM, BN>(p, reinterpret_cast<int*>(smem), wg, m0, n0);
+  }
 }
 
 template <int TM, int TN>
@@ -1034,7 +1042,7 @@ __global__ __launch_bounds__(512) void conv_x3s_kernel(const ConvArgs p) {
         if (m >= p.M || n >= dd.Cout) continue;
         const float4 v = *reinterpret_cast<const float4*>(region + row * W + col);
         if (p.splits > 1) {
-          store_partial(p, m, n, v);
+          store_partial<false>(p, m, n, v);
         } else if (fastv) {
           epilogue_vec(p, m, n, v, r1[u]);
         } else {
@@ -1356,7 +1364,11 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   dim3 grid((unsigned)tiles, 1, a.splits);
   ConvArgs b = a;
   b.counters = splitk_counters_for(a, tiles);
-  if (planes == 3)
+  if (a.splits > 1 && planes == 3)
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true, true>), grid, dim3(64 * WM * WN), 0, s, b);
+  else if (a.splits > 1)
+    hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true, true>), grid, dim3(64 * WM * WN), 0, s, b);
+  else if (planes == 3)
     hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, b);
   else
     hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true>), grid, dim3(64 * WM * WN), 0, s, b);

@@ -92,11 +92,11 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
 // v_cvt_pk_bf16_f32, 8 + 8 unpacks (the low half of a pair is `u << 16`, the high half `u &
 // 0xffff0000`: bf16 → fp32 is exact) and 16 v_sub_f32 — 44 instructions, against ~60 for the
 // element-wise form (hipcc converts element by element, then repacks). Same RNE hi / mid / lo as split8.
-// Round 5: the residual subtractions as packed pairs (f32x2 arithmetic → v_pk_add_f32, two lanes of fp32 per
-// instruction): 12 cvt + 16 unpacks + 8 v_pk_add_f32 = 36 VALU per 8 elements. Same values, bit for bit
-// (an fp32 subtraction is exact here either way). -DSP_SPLIT_PK2=0: the scalar-subtraction form (diagnostic A/B).
+// Round 5 built the residual subtractions as packed pairs (f32x2 arithmetic → v_pk_add_f32: 36 VALU per 8
+// elements instead of 44, bit-identical); it measured 0.3 % slower in the C2 step (same box, alternating,
+// profiles/r5/x3/ab_round5_changes.json), so the scalar form stays. -DSP_SPLIT_PK2=1: the packed form (A/B).
 #ifndef SP_SPLIT_PK2
-#define SP_SPLIT_PK2 1
+#define SP_SPLIT_PK2 0
 #endif
 template <int PL>
 __device__ __forceinline__ void split_frag_pk(const float4& x0, const float4& x1, bf16x8* out) {

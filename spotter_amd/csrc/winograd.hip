@@ -425,10 +425,10 @@ int wino_gemm(const char* what, const sp_conv_desc* d, const uint16_t* wt_wino, 
   // 0.282), 128×128 k32 (245) otherwise (40²×384: 0.308 vs 0.327; 20²×512: 0.140 vs 0.150 for cfg 47).
   int cfg = forced_cfg();
   if (cfg < 0) {
-    // short batches (the bs1 80² maps, 14400 rows): 256×128 with eight 32×128 waves for Cout >= 256 (0.0395 vs
-    // 0.0535 ms for 245 at 80²×384), else 64×64 (0.0103 vs 0.0114 for 246 at 80²×128;
-    // profiles/r5/bs1/tune_bs1_cross.json)
-    if (d->Cout % 128 == 0 && T * NC >= 12000 && T * NC < 40000) cfg = d->Cout >= 256 ? 63 : 14;
+    // short batches (the bs1 80² maps, 14400 rows; not the bs32 20² maps at 28800): 256×128 with eight 32×128
+    // waves for Cout >= 256 (0.0395 vs 0.0535 ms for 245 at 80²×384), else 64×64 (0.0103 vs 0.0114 for 246 at
+    // 80²×128; profiles/r5/bs1/tune_bs1_cross.json)
+    if (d->Cout % 128 == 0 && T * NC >= 12000 && T * NC < 20000) cfg = d->Cout >= 256 ? 63 : 14;
     else if (d->Cout % 128 || T * NC < 12000) cfg = 14;
     else if (T * NC >= 400000 && d->Cout >= 384) cfg = 247;
     else if (d->Cout <= 256) cfg = 246;
