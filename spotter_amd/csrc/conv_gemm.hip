@@ -425,7 +425,9 @@ extern "C" int sp_conv2d(const sp_conv_desc* d, void* stream) {
     cfg = tile_table_lookup(a.M, d->Cout, a.K, d->KH, d->stride, planes);
   if (cfg < 0 && a.splits > 1 && planes && g_forced_splitk_cfg >= 0) cfg = g_forced_splitk_cfg;
   if (planes) return launch_mfma16(a, planes, cfg, s);
-  if (a.splits > 1) return launch<1, 1, 0, 2, false, true>(a, s);
+  if (a.splits > 1 && splitk_counters_for(a, ((a.d.Cout + 63) / 64) * ((a.M + 63) / 64)))
+    return launch<1, 1, 0, 2, false, true>(a, s);  // the in-launch combine (launch<1, 1, 0>: 64×64 tiles)
+  if (a.splits > 1) return launch<1, 1, 0>(a, s);
   switch (cfg) {
     case 220: return launch<2, 2, 0>(a, s);
     case 221: return launch<2, 2, 1>(a, s);

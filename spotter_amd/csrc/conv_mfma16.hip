@@ -1364,9 +1364,9 @@ int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
   dim3 grid((unsigned)tiles, 1, a.splits);
   ConvArgs b = a;
   b.counters = splitk_counters_for(a, tiles);
-  if (a.splits > 1 && planes == 3)
+  if (b.counters && planes == 3)
     hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true, true>), grid, dim3(64 * WM * WN), 0, s, b);
-  else if (a.splits > 1)
+  else if (b.counters)
     hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 1, true, true>), grid, dim3(64 * WM * WN), 0, s, b);
   else if (planes == 3)
     hipLaunchKernelGGL((conv_mfma16_kernel<WM, WN, TM, TN, 3, true>), grid, dim3(64 * WM * WN), 0, s, b);
