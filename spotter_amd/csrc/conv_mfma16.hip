@@ -769,6 +769,10 @@ int launch_pp(const ConvArgs& a, int planes, hipStream_t s) {
 
 
 #endif  // SP_DIAG_KERNELS
+// The staggered (conv_x3s, cfg 70-72) and persistent (conv_x3p, cfg 73-75) split kernels below hold no tile-table
+// entry and lost on every large C2 shape when re-timed in round 5 (1.1-2× the table's tiles,
+// profiles/r5/x3/retune_x3s_x3p.json): diagnostic builds only, like conv_pipe / conv_pp above.
+#if SP_DIAG_KERNELS
 // ---------------------------------------------------------------------------------------------
 // Staggered split-GEMM kernel (x3 / bf16): 8 waves, each owning 32 rows × the whole BN = 32·TN
 // columns of a 256 × BN tile, so every A fragment is split once per workgroup (VALU per MFMA
@@ -1352,6 +1356,7 @@ int launch_x3p(const ConvArgs& a, int planes, hipStream_t s) {
     hipLaunchKernelGGL((conv_x3p_kernel<TN, 1>), dim3(grid), dim3(512), 0, s, a, (int)tiles);
   return check_launch(planes == 3 ? "sp_conv2d(f32x3 persistent)" : "sp_conv2d(bf16 persistent)");
 }
+#endif  // SP_DIAG_KERNELS (x3s / x3p)
 
 template <int WM, int WN, int TM, int TN>
 int launch_cfg(const ConvArgs& a, int planes, hipStream_t s) {
@@ -1424,6 +1429,7 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
     if (rc || a.splits == 1) return rc;
     return launch_splitk_reduce(a, s);
   }
+#if SP_DIAG_KERNELS
   if (cfg >= 70 && cfg <= 75 && (a.d.C_bf16 || a.d.res1_bf16 || a.d.res2_bf16)) cfg = -1;  // register epilogues: fp32 rows only
   if (cfg >= 73 && cfg <= 75 && !a.d.A2 && a.splits == 1 && a.vec_epi) {
     switch (cfg) {
@@ -1439,6 +1445,12 @@ int launch_mfma16(const ConvArgs& a, int planes, int cfg, hipStream_t s) {
       default: return launch_x3s<4>(a, planes, s);  // 256×128
     }
   }
+#else
+  if (cfg >= 70 && cfg <= 75 && !a.d.A2) {
+    set_error("sp_conv2d: tile configuration %d (conv_x3s / conv_x3p) is in the diagnostic build only", cfg);
+    return -1;
+  }
+#endif
 #if SP_DIAG_KERNELS
   if (cfg >= 31 && cfg <= 32 && !a.d.A2) {
     switch (cfg) {

@@ -214,10 +214,11 @@ def _bf16(a):
     return (((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16).astype(np.uint32).view(np.float32)
 
 
-# (21-26 and 31-32, the conv_pipe / conv_pp kernels, are in diagnostic builds only since round 5)
+# (21-26 and 31-32, the conv_pipe / conv_pp kernels, and 70-75, the conv_x3s / conv_x3p kernels, are in diagnostic
+# builds only since round 5)
 MFMA16_CFGS = [None, "1", "2", "3", "4", "5", "6", "11", "12", "13", "14", "15", "16", "17", "18", "19", "20", "33",
                "34", "35", "36", "37", "38", "41", "42", "43", "44", "45", "46", "47", "48", "49", "50", "51", "62", "63",
-               "64", "65", "70", "71", "72", "73", "74", "75"]
+               "64", "65"]
 
 
 @pytest.mark.parametrize("case", CONV_CASES[:7] + [(1, 5, 7, 256, 96, 3, 1, "relu")])

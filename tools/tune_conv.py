@@ -23,7 +23,7 @@ from spotter_amd import ops
 from spotter_amd.ops import view
 
 X3_CFGS = ["-", "11", "12", "13", "14", "16", "17", "33", "41", "42", "43", "44", "45", "46", "47", "49", "50", "51",
-           "62", "63", "64", "65", "70", "71", "72"]
+           "62", "63", "64", "65"]  # (70-75: diagnostic builds only since round 5)
 F32_CFGS = ["-", "110", "111", "120", "121", "210", "211", "220", "221", "4110", "4111", "4210", "4120", "1110", "1111",
             "1120", "1121"]
 
