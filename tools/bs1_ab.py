@@ -1,6 +1,7 @@
 """bs1 forward A/B on hipGraph replays: the split-K launches' tile, split cap and minimum k-tiles
 (sp_set_splitk_config), the split-K combine ("comb": inside the GEMM launch, Engine.splitk_combine; else
-the reduce launch) and the fused post-LayerNorm epilogue (Engine.fuse_ln, diagnostic builds), same process,
+the reduce launch), the fused post-LayerNorm epilogue (Engine.fuse_ln, diagnostic builds) and the decoder's
+small-M linears on the split kernel ("x3dec", a second engine), same process,
 variants interleaved over several rounds.
 
     python tools/bs1_ab.py [--preset r101vd] [--reps 100] [--rounds 3] [--variants plain:-1:16:8,ln:-1,...]
@@ -36,16 +37,30 @@ def main():
     eng = Engine(cfg, generate(cfg, seed=0), dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
-    dflt = ["plain", "-1", "16", "8"]  # plain|comb|ln : split-K tile : max splits : min k-tiles
+    dflt = ["plain", "-1", "16", "8"]  # plain|comb|ln|x3dec : split-K tile : max splits : min k-tiles
     variants = [(lambda q: q + dflt[len(q):])(v.split(":")) for v in a.variants.split(",")]
     runners, ref = {}, None
     res = {}
+    eng_x3 = None
     for mode, c, ms, mk in variants:
-        eng.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
-        eng.splitk_combine = mode == "comb"  # "comb": split-K combined inside the GEMM launch
+        if mode == "x3dec":  # the decoder's small-M linears on the split kernel instead of the fp32 MFMA
+            if eng_x3 is None:
+                import spotter_amd.engine as em
+
+                saved = em._X3_FASTER
+                em._X3_FASTER = saved | {(n, k, True) for n in range(129, 4097) for k in (256, 512, 1024)}
+                try:
+                    eng_x3 = Engine(cfg, generate(cfg, seed=0), dev)
+                finally:
+                    em._X3_FASTER = saved
+            eng_run = eng_x3
+        else:
+            eng_run = eng
+        eng_run.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
+        eng_run.splitk_combine = mode == "comb"  # "comb": split-K combined inside the GEMM launch
         ops.force_splitk_config(c, int(ms), int(mk))
         try:
-            r = GraphRunner(eng, 1, cfg.image_size, cfg.image_size)
+            r = GraphRunner(eng_run, 1, cfg.image_size, cfg.image_size)
         finally:
             ops.force_splitk_config(None)
         lg, bx = r(x)
