@@ -37,7 +37,7 @@ def main():
     eng = Engine(cfg, generate(cfg, seed=0), dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.rand((1, 3, cfg.image_size, cfg.image_size), device=dev, generator=g)
-    dflt = ["plain", "-1", "16", "8"]  # plain|comb|ln|x3dec : split-K tile : max splits : min k-tiles
+    dflt = ["plain", "-1", "16", "8"]  # plain|comb|ln|x3dec|w<n> : split-K tile : max splits : min k-tiles
     variants = [(lambda q: q + dflt[len(q):])(v.split(":")) for v in a.variants.split(",")]
     runners, ref = {}, None
     res = {}
@@ -56,6 +56,8 @@ def main():
             eng_run = eng_x3
         else:
             eng_run = eng
+        # "w<n>": the F(4x4) Winograd size gate at pixels x Cin >= 2^n (Engine.WINO43_MIN_WORK; default 2^19)
+        eng_run.WINO43_MIN_WORK = 1 << int(mode[1:]) if mode[:1] == "w" else Engine.WINO43_MIN_WORK
         eng_run.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
         eng_run.splitk_combine = mode == "comb"  # "comb": split-K combined inside the GEMM launch
         ops.force_splitk_config(c, int(ms), int(mk))
