@@ -23,11 +23,28 @@ constexpr int KT = 64;  // keys per LDS tile
 // (__builtin_amdgcn_exp2f, one instruction instead of expf's range-reduced sequence): the same softmax, within
 // 1e-6 of an fp64 reference like the expf form, 1.17-1.28x faster on the C2 / C3 shapes
 // (profiles/r4/attn_exp2_ab.jsonl).
+// Workgroup → (q-tile, head, image), grouped by XCD: workgroups are dealt round-robin over the 8 XCDs
+// (MI355X_MICROARCH.md), so with the q-tile index fastest in the launch order the q-tiles of one (image, head)
+// landed on different XCDs and each XCD's L2 fetched that head's K / V on its own. Here XCD x takes the x-th
+// contiguous chunk of the work list (q-tile fastest), so the q-tiles of a head share one L2: 1.02-1.04x (fp32)
+// and 1.07-1.11x (bf16) at bs32 / bs128, bit-identical (profiles/r5/attn/xcd_*.jsonl). Grids under 512
+// workgroups (bs1-bs8) keep the launch order, where grouping measured 1-3 % slower.
+__device__ __forceinline__ void attn_work(int n, int heads, int& qtile, int& hh, int& b) {
+  const int total = gridDim.x, L = blockIdx.x;
+  const int per = total >> 3, rem = total & 7, x = L & 7, i = L >> 3;
+  const int w = total < 512 ? L : (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + i;
+  const int qt = (n + 63) / 64;
+  qtile = w % qt;
+  const int r = w / qt;
+  hh = r % heads;
+  b = r / heads;
+}
+
 template <int DH>
 __global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict__ q, int64_t ldq,
                                                         const float* __restrict__ k, int64_t ldk,
                                                         const float* __restrict__ v, int64_t ldv,
-                                                        float* __restrict__ o, int64_t ldo, int n,
+                                                        float* __restrict__ o, int64_t ldo, int n, int heads,
                                                         float scale) {  // scale: including log2 e
   static_assert(DH % 16 == 0, "head dim in 16-channel blocks");
   constexpr int LD = DH + 4;     // padded LDS row (floats): 16 key rows → distinct bank groups
@@ -40,10 +57,10 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict_
   const int lane = tid & 63;
   const int c16 = lane & 15;
   const int g = lane >> 4;
-  const int b = blockIdx.z;
-  const int hh = blockIdx.y;
+  int qtile, hh, b;
+  attn_work(n, heads, qtile, hh, b);
   const int64_t rowbase = (int64_t)b * n;
-  const int q0 = blockIdx.x * 64 + wave * 16;
+  const int q0 = qtile * 64 + wave * 16;
   const int qi = q0 + c16;
   // B operand of Sᵀ = K Qᵀ: step s, lane group g supplies channel g·QS + s of query qi.
   float qv[QS];
@@ -145,7 +162,7 @@ template <int DH>
 __global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict__ q, int64_t ldq,
                                                         const float* __restrict__ k, int64_t ldk,
                                                         const float* __restrict__ v, int64_t ldv,
-                                                        float* __restrict__ o, int64_t ldo, int n,
+                                                        float* __restrict__ o, int64_t ldo, int n, int heads,
                                                         float scale) {  // scale: including log2 e
   static_assert(DH % 16 == 0, "head dim in 16-channel blocks");
   constexpr int LK = DH + 8;   // K tile row (bf16): 16 rows of a read land on distinct bank pairs
@@ -159,10 +176,10 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict_
   const int lane = tid & 63;
   const int c16 = lane & 15;
   const int g = lane >> 4;
-  const int b = blockIdx.z;
-  const int hh = blockIdx.y;
+  int qtile, hh, b;
+  attn_work(n, heads, qtile, hh, b);
   const int64_t rowbase = (int64_t)b * n;
-  const int qi = blockIdx.x * 64 + wave * 16 + c16;
+  const int qi = qtile * 64 + wave * 16 + c16;
   bf16x4_s qv[QC];  // channels 16c + 4g .. +3 of query qi
   {
     const float* qr = q + (rowbase + (qi < n ? qi : n - 1)) * ldq + hh * DH + 4 * g;
@@ -242,12 +259,17 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict_
 template <int DH, bool BF>
 int launch(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v, int64_t ldv,
            float* o, int64_t ldo, int batch, int n, int heads, float scale, hipStream_t s) {
-  dim3 grid((n + 63) / 64, heads, batch);
+  const int64_t wgs = (int64_t)((n + 63) / 64) * heads * batch;  // one workgroup per 64 queries of a head
+  if (wgs > 0x7fffffff) {
+    set_error("sp_attention: %lld workgroups", (long long)wgs);
+    return -1;
+  }
+  dim3 grid((unsigned)wgs);
   if constexpr (BF)
-    hipLaunchKernelGGL((attn_bf16_kernel<DH>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n,
+    hipLaunchKernelGGL((attn_bf16_kernel<DH>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n, heads,
                        scale * 1.4426950408889634f);  // log2 e: the softmax in base 2
   else
-    hipLaunchKernelGGL((attn_mfma_kernel<DH>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n,
+    hipLaunchKernelGGL((attn_mfma_kernel<DH>), grid, dim3(256), 0, s, q, ldq, k, ldk, v, ldv, o, ldo, n, heads,
                        scale * 1.4426950408889634f);
   return check_launch(BF ? "sp_attention_bf16" : "sp_attention");
 }
