@@ -1,0 +1,9 @@
+# maxpool XCD-grouping A/B: old (_ab/lib_old.so) vs new library, alternating processes, then the pool tests
+set -o pipefail
+O=gpurun_out/pool; mkdir -p $O
+for t in old new old new; do
+  if [ $t = old ]; then L=$PWD/_ab/lib_old.so; else L=$PWD/spotter_amd/libspotter_hip.so; fi
+  SPOTTER_HIP_LIB=$L timeout -k 10 180 python -u tools/microbench/pool_ab.py --tag $t > $O/$t.$RANDOM.jsonl || exit 1
+done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -k "pool" > $O/tests.log 2>&1 || exit 1
+echo done
