@@ -1,4 +1,4 @@
-"""sp_maxpool3x3s2 (fp32 and bf16 rows) on the stem shapes of C2 (bs32, 320² × 64, fp32) and C3 (bs256, bf16),
+"""sp_maxpool3x3s2 and sp_upsample2x_nearest (fp32 and bf16 rows) on the stem shapes of C2 (bs32, 320² × 64, fp32) and C3 (bs256, bf16),
 timed with HIP events, plus a sha256 of each output, so two libraries (SPOTTER_HIP_LIB) can be compared for
 bit-identical results and time in alternating processes on one box.
 
@@ -47,6 +47,29 @@ def main():
         ms = e0.elapsed_time(e1) / a.reps
         nbytes = x.element_size() * n * c * (h * w + ho * wo)
         e = {"shape": [n, h, w, c, "bf16" if bf else "f32"], "us": round(ms * 1e3, 2),
+             "TBps": round(nbytes / ms / 1e9, 2), "sha": hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest()[:16]}
+        res.append(e)
+        print(json.dumps(e), flush=True)
+        del x, y
+    # nearest ×2 upsample into the channel slice of a concat buffer (the CCFM's top-down path): C2 fp32, C3 bf16
+    for (n, h, w, c, bf) in [(32, 20, 20, 256, False), (32, 40, 40, 256, False), (256, 40, 40, 256, True),
+                             (256, 20, 20, 256, True)]:
+        dt = torch.int16 if bf else torch.float32
+        x = torch.randn(n * h * w * c, device=dev, generator=g).to(dt)
+        y = torch.zeros(n * 4 * h * w * 2 * c, dtype=dt, device=dev)
+        run = lambda: ops.upsample2x(ops.V(x, 0, c), ops.V(y, 0, 2 * c), n, h, w, c)  # noqa: E731
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.reps):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.reps
+        nbytes = x.element_size() * n * h * w * c * 5
+        e = {"shape": ["up", n, h, w, c, "bf16" if bf else "f32"], "us": round(ms * 1e3, 2),
              "TBps": round(nbytes / ms / 1e9, 2), "sha": hashlib.sha256(y.cpu().numpy().tobytes()).hexdigest()[:16]}
         res.append(e)
         print(json.dumps(e), flush=True)
