@@ -17,20 +17,28 @@ inline unsigned grid_for(int64_t work, int block = 256) {
   return (unsigned)g;
 }
 
-// c4 = channels / 4. Output rows (b, oy) over blockIdx.y (strided past 65535), wo·c4 float4s across blockIdx.x ×
-// threads: 32-bit index math only (the grid-stride form's 64-bit divisions dominated at 4.7 TB/s).
+// c4 = channels / 4. Chunks of MP_ROWS output rows of one image over blockIdx.y (strided past 65535), wo·c4 float4s
+// across blockIdx.x × threads, 32-bit index math (the grid-stride form's 64-bit divisions dominated at 4.7 TB/s).
+// A thread walks its chunk's rows top-down: the 3-tap row maximum of input row 2·oy + 1 is kept for output row
+// oy + 1, so each output reads 6 input float4s instead of 9. max is exact, so any order gives the same bits.
+// rpc (rows per chunk) = MP_ROWS on large maps (1.04-1.05x at C2 / C3, profiles/r5/pool/rowwalk_*), 1 where
+// the chunks would leave the grid short of workgroups (bs1: 0.75x with 4).
+constexpr int MP_ROWS = 4;
+inline int maxpool_rows_per_chunk(int n, int ho, int gx) {
+  return (int64_t)n * ho * gx >= 16384 ? MP_ROWS : 1;  // >= 16 workgroups per CU with the chunks
+}
+
 __global__ __launch_bounds__(256) void maxpool3s2_kernel(const float4* __restrict__ x, float4* __restrict__ y,
-                                                         int n, int h, int w, int c4, int ho, int wo, int64_t ldy4) {
+                                                         int n, int h, int w, int c4, int ho, int wo, int64_t ldy4,
+                                                         int rpc) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= wo * c4) return;
   const int ox = j / c4, cc = j - ox * c4;
-  for (int row = blockIdx.y; row < n * ho; row += gridDim.y) {  // row = b * ho + oy
-  const int oy = row % ho, b = row / ho;
-  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-#pragma unroll
-  for (int dy = 0; dy < 3; ++dy) {
-    const int iy = oy * 2 - 1 + dy;
-    if ((unsigned)iy >= (unsigned)h) continue;
+  const int chunks = (ho + rpc - 1) / rpc;
+  const float4 ninf = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  auto hmax = [&](int b, int iy) {  // max over the 3 taps of input row iy (-inf outside the map)
+    float4 m = ninf;
+    if ((unsigned)iy >= (unsigned)h) return m;
     const float4* xr = x + ((int64_t)b * h + iy) * w * c4 + cc;
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
@@ -39,8 +47,20 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const float4* __restric
       const float4 v = xr[ix * c4];
       m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
     }
-  }
-  y[((int64_t)row * wo + ox) * ldy4 + cc] = m;
+    return m;
+  };
+  for (int ch = blockIdx.y; ch < n * chunks; ch += gridDim.y) {
+    const int b = ch / chunks, oy0 = (ch - b * chunks) * rpc;
+    const int oy1 = oy0 + rpc < ho ? oy0 + rpc : ho;
+    float4 prev = hmax(b, 2 * oy0 - 1);
+    for (int oy = oy0; oy < oy1; ++oy) {
+      const float4 r0 = hmax(b, 2 * oy), r1 = hmax(b, 2 * oy + 1);
+      float4 m;
+      m.x = fmaxf(fmaxf(prev.x, r0.x), r1.x); m.y = fmaxf(fmaxf(prev.y, r0.y), r1.y);
+      m.z = fmaxf(fmaxf(prev.z, r0.z), r1.z); m.w = fmaxf(fmaxf(prev.w, r0.w), r1.w);
+      y[(((int64_t)b * ho + oy) * wo + ox) * ldy4 + cc] = m;
+      prev = r1;
+    }
   }
 }
 
@@ -94,31 +114,43 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 
 __global__ __launch_bounds__(256) void maxpool3s2_bf16_kernel(const uint4* __restrict__ x, uint4* __restrict__ y,
                                                               int n, int h, int w, int c8, int ho, int wo,
-                                                              int64_t ldy8) {
+                                                              int64_t ldy8, int rpc) {
+  // the fp32 kernel's row walk (rpc output rows per chunk, one 3-tap row maximum carried between rows)
   const int j = blockIdx.x * 256 + threadIdx.x;
   if (j >= wo * c8) return;
   const int ox = j / c8, cc = j - ox * c8;
-  for (int row = blockIdx.y; row < n * ho; row += gridDim.y) {
-    const int oy = row % ho, b = row / ho;
-    float m[8];
+  const int chunks = (ho + rpc - 1) / rpc;
+  auto hmax = [&](int b, int iy, float* m) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    if ((unsigned)iy >= (unsigned)h) return;
+    const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      const int iy = oy * 2 - 1 + dy;
-      if ((unsigned)iy >= (unsigned)h) continue;
-      const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ix = ox * 2 - 1 + dx;
+      if ((unsigned)ix >= (unsigned)w) continue;
+      float f[8];
+      unpack8(xr[ix * c8], f);
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int ix = ox * 2 - 1 + dx;
-        if ((unsigned)ix >= (unsigned)w) continue;
-        float f[8];
-        unpack8(xr[ix * c8], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
-      }
+      for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], f[e]);
     }
-    y[((int64_t)row * wo + ox) * ldy8 + cc] = pack8(m);  // exact: every max is a bf16 value
+  };
+  for (int ch = blockIdx.y; ch < n * chunks; ch += gridDim.y) {
+    const int b = ch / chunks, oy0 = (ch - b * chunks) * rpc;
+    const int oy1 = oy0 + rpc < ho ? oy0 + rpc : ho;
+    float prev[8], r0[8], r1[8];
+    hmax(b, 2 * oy0 - 1, prev);
+    for (int oy = oy0; oy < oy1; ++oy) {
+      hmax(b, 2 * oy, r0);
+      hmax(b, 2 * oy + 1, r1);
+      float m[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        m[e] = fmaxf(fmaxf(prev[e], r0[e]), r1[e]);
+        prev[e] = r1[e];
+      }
+      y[(((int64_t)b * ho + oy) * wo + ox) * ldy8 + cc] = pack8(m);  // exact: every max is a bf16 value
+    }
   }
 }
 
@@ -383,9 +415,12 @@ extern "C" int sp_maxpool3x3s2(const float* x, float* y, int64_t ldy, int n, int
                "sp_maxpool3x3s2: bad args");
   int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   SP_ARG_CHECK((int64_t)n * ho < (1 << 30) && (int64_t)wo * (c / 4) < (1 << 30), "sp_maxpool3x3s2: size out of range");
-  const int gy = n * ho < 65535 ? n * ho : 65535;
-  hipLaunchKernelGGL(maxpool3s2_kernel, dim3((wo * (c / 4) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
-                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4);
+  const int gx = (wo * (c / 4) + 255) / 256;
+  const int rpc = maxpool_rows_per_chunk(n, ho, gx);
+  const int64_t rows = (int64_t)n * ((ho + rpc - 1) / rpc);
+  const int gy = rows < 65535 ? (int)rows : 65535;
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(gx, gy), dim3(256), 0, as_stream(stream),
+                     (const float4*)x, (float4*)y, n, h, w, c / 4, ho, wo, ldy / 4, rpc);
   return check_launch("sp_maxpool3x3s2");
 }
 
@@ -409,9 +444,12 @@ extern "C" int sp_maxpool3x3s2_bf16(const uint16_t* x, uint16_t* y, int64_t ldy,
                "sp_maxpool3x3s2_bf16: bad args");
   int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   SP_ARG_CHECK((int64_t)n * ho < (1 << 30) && (int64_t)wo * (c / 8) < (1 << 30), "sp_maxpool3x3s2_bf16: size out of range");
-  const int gy = n * ho < 65535 ? n * ho : 65535;
-  hipLaunchKernelGGL(maxpool3s2_bf16_kernel, dim3((wo * (c / 8) + 255) / 256, gy), dim3(256), 0, as_stream(stream),
-                     (const uint4*)x, (uint4*)y, n, h, w, c / 8, ho, wo, ldy / 8);
+  const int gx = (wo * (c / 8) + 255) / 256;
+  const int rpc = maxpool_rows_per_chunk(n, ho, gx);
+  const int64_t rows = (int64_t)n * ((ho + rpc - 1) / rpc);
+  const int gy = rows < 65535 ? (int)rows : 65535;
+  hipLaunchKernelGGL(maxpool3s2_bf16_kernel, dim3(gx, gy), dim3(256), 0, as_stream(stream),
+                     (const uint4*)x, (uint4*)y, n, h, w, c / 8, ho, wo, ldy / 8, rpc);
   return check_launch("sp_maxpool3x3s2_bf16");
 }
 

@@ -769,8 +769,11 @@ def test_pools_and_upsample_exact(dev):
     from spotter_amd.ops import V
 
     rng = np.random.default_rng(3)
-    # (4100, 16, 1, 4): more than 65535 input / output rows, so the row-strided grids loop
-    for (n, h, w, c) in [(2, 9, 7, 8), (1, 16, 16, 64), (3, 5, 6, 4), (4100, 16, 1, 4)]:
+    # (4100, 16, 1, 4) / (70000, 2, 1, 4): more than 65535 input rows / output row chunks, so the row-strided
+    # grids loop
+    # (2000, 20, 3, 8): the max pool's 4-row chunks with a partial last chunk (ho = 10)
+    for (n, h, w, c) in [(2, 9, 7, 8), (1, 16, 16, 64), (3, 5, 6, 4), (4100, 16, 1, 4), (70000, 2, 1, 4),
+                         (2000, 20, 3, 8)]:
         x = rng.standard_normal((n, h, w, c)).astype(np.float32)
         xt = T(x.reshape(-1), dev)
         ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1

@@ -1,7 +1,7 @@
 # Pool / upsample A/B: the previous library (_ab/lib_old.so, copied in by hand) vs the in-tree one, alternating
 # processes on one box, then the pool / upsample GPU tests. Run on the GPU box from the repo root.
 set -o pipefail
-O=gpurun_out/up; mkdir -p $O
+O=gpurun_out/${1:-up}; mkdir -p $O
 for t in old new old new; do
   if [ $t = old ]; then L=$PWD/_ab/lib_old.so; else L=$PWD/spotter_amd/libspotter_hip.so; fi
   SPOTTER_HIP_LIB=$L timeout -k 10 180 python -u tools/microbench/pool_ab.py --tag $t > $O/$t.$RANDOM.jsonl || exit 1
