@@ -114,3 +114,21 @@ R18VD = SpotterConfig(
     decoder_in_channels=[256, 256, 256], decoder_layers=3, hidden_expansion=0.5,
 )
 PRESETS = {"r101vd": R101VD, "r18vd": R18VD}
+
+# Engine precision names → (conv GEMM operand mode, linear GEMM operand mode); engine.py documents the modes.
+# Here (no GPU import) so the drop-in can refuse an unknown SPOTTER_PRECISION at serve.py import time.
+PRECISIONS = {
+    "fp32": ("x3", "x3"),
+    "fp32-mfma": ("f32", "f32"),
+    "bf16": ("bf16", "bf16"),
+    "bf16-convs": ("bf16", "x3"),
+    "bf16-all": ("bf16", "bf16"),  # round-2 name of "bf16"
+}
+PRECISION_ENV = "SPOTTER_PRECISION"
+
+
+def check_precision(precision: str) -> str:
+    """A PRECISIONS key, else ValueError naming the accepted values (and the env variable that set it)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision {precision!r} (e.g. from {PRECISION_ENV}) must be one of {sorted(PRECISIONS)}")
+    return precision

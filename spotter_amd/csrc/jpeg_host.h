@@ -15,6 +15,9 @@
 
 #include "../../include/spotter_hip.h"
 
+// libjpeg(-turbo)'s JPEG_MAX_DIMENSION (jmorecfg.h): larger frames raise JERR_IMAGE_TOO_BIG on load and save
+#define SP_JPEG_MAX_DIMENSION 65500
+
 namespace sp {
 
 void set_error(const char* fmt, ...);
@@ -413,6 +416,8 @@ struct Decoder {
     const int H = (q[1] << 8) | q[2], W = (q[3] << 8) | q[4];
     nc = q[5];
     if (H <= 0 || W <= 0) return bad("zero image size (DNL) or bad header");
+    // libjpeg's JPEG_MAX_DIMENSION (jmorecfg.h): jdinput.c initial_setup raises JERR_IMAGE_TOO_BIG above it
+    if (H > SP_JPEG_MAX_DIMENSION || W > SP_JPEG_MAX_DIMENSION) return bad("image wider or higher than 65500");
     if (nc != 1 && nc != 3) return bad("component count other than 1 or 3");
     if (L != 6 + 3 * nc) return bad("SOF length does not match its component count");  // JERR_BAD_LENGTH
     int maxh = 1, maxv = 1;
@@ -727,7 +732,8 @@ constexpr EncHuff derive_enc(const uint8_t (&bits)[16], const uint8_t* vals) {
 constexpr int64_t kMaxBitsPerBlock = 22 + 63 * 26 + 16;
 
 inline int enc_plan(int32_t W, int32_t H, int32_t quality, int32_t subsampling, sp_jpeg_enc_layout* L) {
-  if (W <= 0 || H <= 0 || W > 65535 || H > 65535) return -1;
+  // jcinit / jcmaster.c initial_setup: JERR_IMAGE_TOO_BIG above JPEG_MAX_DIMENSION; the caller falls back to Pillow
+  if (W <= 0 || H <= 0 || W > SP_JPEG_MAX_DIMENSION || H > SP_JPEG_MAX_DIMENSION) return -1;
   if (quality != -1 && (quality < 1 || quality > 100)) return -1;
   int h0, v0;
   switch (subsampling) {  // Pillow's codes (JpegEncode.c): -1 keeps libjpeg's default 2x2

@@ -64,6 +64,11 @@ class _MemoFont(_PILFont.FreeTypeFont):
                 self._exact.popitem(last=False)
 
     def getmask2(self, text, mode="", *args, start=None, **kwargs):
+        if mode not in ("", "L", "1"):
+            # "RGBA" (ImageDraw.text(embedded_color=True)): Pillow fills the returned mask's alpha band in place
+            # (color.fillband), so a shared cached mask would be overwritten; these renders are never cached
+            self.memo_stats["bypass"] += 1
+            return super().getmask2(text, mode, *args, start=start, **kwargs)
         key = ekey = None
         if not args and isinstance(text, str) and start is not None:
             try:

@@ -5,7 +5,9 @@ time and by tests/test_dropin_reference.py in memory, so the image and the test 
 
 Only module-scope lines change; the Ray Serve deployment class AmenitiesDetector (serve.py:64-196) stays the
 reference's text byte for byte (tests/test_dropin_reference.py compares it). The model and processor built
-at import (serve.py:203-204) become the spotter_amd objects, and serve.py's module-global `Image` (bound by
+at import (serve.py:203-204) become the spotter_amd objects (the model's operand precision from the
+SPOTTER_PRECISION environment variable, default "fp32"; an unknown value fails the import; serve.py already
+imports os, :5), and serve.py's module-global `Image` (bound by
 `from PIL import Image, ImageDraw`, serve.py:10) is rebound to spotter_amd.jpeg.image_module(): Pillow's
 module with a GPU `open` (JPEGs decoded on the GPU, pixels identical to Pillow's; Pillow parses the header
 first, so every file Pillow refuses raises exactly as before) whose decoded images also encode on the GPU
@@ -26,9 +28,12 @@ NEW_MODEL = ("from spotter_amd import SpotterForObjectDetection, SpotterImagePro
              "from spotter_amd.jpeg import image_module\n"
              "Image = image_module()  # PIL.Image with the GPU JPEG decode / encode (AmenitiesDetector unchanged)\n"
              "ImageDraw = draw_module()  # PIL.ImageDraw whose default font memoises its glyph masks\n"
-             "model = SpotterForObjectDetection.from_pretrained(model_name).to(device)")
+             "model = SpotterForObjectDetection.from_pretrained(\n"
+             "    model_name, precision=os.environ.get(\"SPOTTER_PRECISION\", \"fp32\")  # fp32 (parity) or bf16 (C4)\n"
+             ").to(device)")
 NEW_PROC = "processor = SpotterImageProcessor.from_pretrained(model_name)"
 MARK = "from spotter_amd import SpotterForObjectDetection"
+PRECISION_ARG = 'precision=os.environ.get("SPOTTER_PRECISION", "fp32")'
 REPLACEMENTS = ((OLD_MODEL, NEW_MODEL), (OLD_PROC, NEW_PROC))
 
 
@@ -49,7 +54,7 @@ def patch_source(src: str) -> str:
 def check(src: str) -> None:
     """The patched file builds the model and processor from spotter_amd and rebinds Image at module scope."""
     if (MARK not in src or NEW_PROC not in src or "Image = image_module()" not in src
-            or "ImageDraw = draw_module()" not in src
+            or "ImageDraw = draw_module()" not in src or PRECISION_ARG not in src
             or any(old in src for old, _ in REPLACEMENTS)):
         raise ValueError("serve.py is not the spotter_amd drop-in")
 

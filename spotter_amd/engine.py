@@ -31,7 +31,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .config import SpotterConfig
+from .config import PRECISIONS, SpotterConfig, check_precision
 from .ops import V, view
 from .weights import backbone_plan
 
@@ -61,13 +61,7 @@ _X3_FASTER = {(256, 64, False), (256, 1024, True), (1024, 256, True), (512, 256,
 # bs32): recall 0.971, p95 |dscore| 0.012, AP 0.958 — closer than round 2's bf16 mode with x3 linears and
 # a bf16 stem (0.906 / 0.052 / 0.916: the bf16-rounded raw pixels of the stem conv were most of the error),
 # at 1.07x (C2) / 1.10x (C3) its speed. "bf16-convs" keeps the linears on the fp32-accurate split.
-PRECISIONS = {
-    "fp32": ("x3", "x3"),
-    "fp32-mfma": ("f32", "f32"),
-    "bf16": ("bf16", "bf16"),
-    "bf16-convs": ("bf16", "x3"),
-    "bf16-all": ("bf16", "bf16"),  # round-2 name of "bf16"
-}
+# The precision names and their (conv, linear) operand modes: config.PRECISIONS.
 
 
 def _wkw(wq):
@@ -157,8 +151,7 @@ class Engine:
                  direct_c64_bf16: bool = True, splitk_combine: bool = False):
         from ._lib import lib
 
-        if precision not in PRECISIONS:
-            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}")
+        check_precision(precision)
         self.cfg = cfg
         self.fold_repvgg = fold_repvgg
         self.fuse_shortcut = fuse_shortcut  # bottleneck tail + projection shortcut as one GEMM (_fused_tail)

@@ -22,6 +22,9 @@ import torch
 from ._lib import SP_JPEG_UNSUPPORTED, SpJpegEncLayout, SpJpegLayout, lib
 
 
+JPEG_MAX_DIMENSION = 65500  # libjpeg's jmorecfg.h limit (csrc/jpeg_host.h SP_JPEG_MAX_DIMENSION)
+
+
 class UnsupportedJpeg(ValueError):
     """A JPEG form (or another format) the GPU decoder does not implement, or a malformed file: either way the
     bytes go to Pillow, i.e. to the reference's own decoder and its own errors and warnings."""
@@ -389,6 +392,8 @@ def _gpu_jpeg_options(im, fp, format, params):
     if format is None or str(format).upper() not in ("JPEG", "JPG") or not hasattr(fp, "write"):
         return None
     if im.mode != "RGB" or set(params) - {"quality", "subsampling"}:
+        return None
+    if max(im.size) > JPEG_MAX_DIMENSION:  # libjpeg raises JERR_IMAGE_TOO_BIG: Pillow's save raises it
         return None
     q = params.get("quality", -1)
     sub = params.get("subsampling", -1)

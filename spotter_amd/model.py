@@ -15,7 +15,7 @@ from dataclasses import dataclass
 
 import torch
 
-from .config import PRESETS, SpotterConfig
+from .config import PRESETS, SpotterConfig, check_precision
 
 
 @dataclass
@@ -60,7 +60,9 @@ class SpotterForObjectDetection:
         self.max_wait_ms = max_wait_ms
         self._batcher = None
         self.use_graphs = use_graphs
-        self.precision = precision  # engine.PRECISIONS key; "fp32" = the fp32-accurate parity path
+        # config.PRECISIONS key; "fp32" = the fp32-accurate parity path, "bf16" = the C4 variant. Checked here, at
+        # construction (serve.py import time), so a bad SPOTTER_PRECISION fails the deployment, not the first request.
+        self.precision = check_precision(precision)
         self._graphs = {}
         self._seen = set()
         self.config = _Config(cfg)
@@ -73,12 +75,17 @@ class SpotterForObjectDetection:
     # -- construction -------------------------------------------------------------
     @classmethod
     def from_pretrained(cls, name_or_path: str = "PekingU/rtdetr_v2_r101vd", synthetic: bool = False,
-                        revision: str = "main", **kw):
+                        revision: str = "main", precision: str = "fp32", **kw):
         """What HF `from_pretrained` loads, offline: a local checkpoint directory, or a hub repo id
         resolved to its snapshot in the local HF cache (the reference image pre-fetches MODEL_NAME
         there: apps/spotter/Dockerfile:17 → download.py:23-27). A name that resolves to nothing
         raises OSError, as HF does offline. Deterministic synthetic weights only on explicit opt-in:
-        `synthetic=True`, or a name of the form "synthetic:<preset>" (e.g. via MODEL_NAME)."""
+        `synthetic=True`, or a name of the form "synthetic:<preset>" (e.g. via MODEL_NAME).
+        precision: the engine's operand precision (config.PRECISIONS); the drop-in serve.py passes
+        os.environ.get("SPOTTER_PRECISION", "fp32") (deploy/rayservice-template.yaml sets "bf16" for C4).
+        HF's own from_pretrained has no such input; the weights loaded are the same either way."""
+        check_precision(precision)
+        kw["precision"] = precision
         if name_or_path.startswith("synthetic:"):
             synthetic, name_or_path = True, name_or_path[len("synthetic:"):]
         if synthetic:

@@ -97,3 +97,21 @@ def test_exact_repeats_are_cached_and_bounded():
     for i in range(20):  # distinct strings: no class-memo hits, every render enters the exact cache
         f.getmask2(f"bed {i}", "L", start=(0.3, 0.3), **kw)
     assert len(f._exact) == 8 and ("bed 19", "L", 0.3, 0.3) == next(reversed(f._exact))[:4]
+
+
+def test_embedded_color_text_is_never_served_from_the_memo():
+    """ImageDraw.text(embedded_color=True) on an RGBA image asks for an "RGBA" mask and Pillow then writes the
+    ink alpha into that mask in place (color.fillband): a cached mask would be changed under the memo. Such
+    renders bypass both caches, so repeated and differently coloured labels draw Pillow's pixels."""
+    from spotter_amd.draw import draw_module
+
+    shim = draw_module()
+    a, b = Image.new("RGBA", (160, 60), (10, 20, 30, 255)), Image.new("RGBA", (160, 60), (10, 20, 30, 255))
+    da, db = ImageDraw.Draw(a), shim.Draw(b)
+    for i, fill in enumerate(("white", (255, 0, 0, 128), "white", (0, 255, 0, 40))):
+        for d in (da, db):
+            d.text(xy=(5.25, 5 + 12 * i), text="sofa", fill=fill, embedded_color=True)
+            d.text(xy=(5.25, 5 + 12 * i), text="sofa", fill=fill, embedded_color=True, stroke_width=1,
+                   stroke_fill="black")
+        assert np.array_equal(np.asarray(a), np.asarray(b)), i
+    assert not any(k[1] == "RGBA" for k in shim.Draw(b).font._exact)

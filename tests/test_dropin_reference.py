@@ -189,3 +189,45 @@ def test_reference_process_single_image_flow_with_our_types(monkeypatch, tmp_pat
     assert [d.label for d in res.detections] == ["TV", "sofa"]
     assert res.detections[0].box == pytest.approx([480.0, 286.8, 720.0, 430.2], abs=1e-3)
     assert len(res.labeled_image_base64) > 500
+
+
+def _template_env(container: str) -> dict:
+    """The env of one container of deploy/rayservice-template.yaml, rendered as spotter-manager renders it."""
+    import yaml
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = open(os.path.join(root, "deploy", "rayservice-template.yaml")).read()
+    body = "\n".join(l for l in src.splitlines() if not l.lstrip().startswith("#"))
+    rc = yaml.safe_load(body.replace("{{.DockerImage}}", "img"))["spec"]["rayClusterConfig"]
+    conts = list(rc["headGroupSpec"]["template"]["spec"]["containers"])
+    for wg in rc["workerGroupSpecs"]:
+        conts += wg["template"]["spec"]["containers"]
+    (c,) = [c for c in conts if c["name"] == container]
+    return {e["name"]: e["value"] for e in c.get("env", [])}
+
+
+@pytest.mark.parametrize("pod", ["ray-head", "ray-worker"])
+def test_rendered_template_configures_a_bf16_engine(monkeypatch, tmp_path, pod):
+    """C4 as deployed: the env of each pod of the rendered template, the reference serve.py with the drop-in
+    applied, imported as Serve imports it; the bound model (pickled, as Ray ships it to a replica) carries
+    precision "bf16", which the engine maps to bf16 conv and linear operands (config.PRECISIONS)."""
+    from spotter_amd.config import PRECISIONS
+
+    env = _template_env(pod)
+    assert env["SPOTTER_PRECISION"] == "bf16"
+    monkeypatch.setenv("SPOTTER_PRECISION", env["SPOTTER_PRECISION"])
+    serve, _ = _load_patched_serve(monkeypatch, tmp_path)
+    assert serve.model.precision == "bf16"
+    (m, _p), _ = pickle.loads(serve.deployment[2])
+    assert m.precision == "bf16" and PRECISIONS[m.precision] == ("bf16", "bf16") and m._engine is None
+
+
+def test_default_and_unknown_precision(monkeypatch, tmp_path):
+    """Without SPOTTER_PRECISION the drop-in keeps the fp32 parity path; an unknown value fails serve.py's
+    import (the deployment does not come up) instead of the first request."""
+    monkeypatch.delenv("SPOTTER_PRECISION", raising=False)
+    serve, _ = _load_patched_serve(monkeypatch, tmp_path)
+    assert serve.model.precision == "fp32"
+    monkeypatch.setenv("SPOTTER_PRECISION", "fp16")
+    with pytest.raises(ValueError, match="SPOTTER_PRECISION"):
+        _load_patched_serve(monkeypatch, tmp_path / "again")

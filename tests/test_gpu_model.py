@@ -112,16 +112,19 @@ def run_case(preset, tag=None, precision="fp32", model=None):
     return model
 
 
-def run_tiled_batch(preset, reps, precision, **engine_kw):
+def run_tiled_batch(preset, reps, precision, model=None, **engine_kw):
     """The golden images tiled `reps` times into ONE batch through the drop-in model (eager, the engine's
     default micro-batch split: the path bench.py times) → (model, golden, post-processed dets, logits,
-    boxes, topk). engine_kw: Engine options other than the product defaults (e.g. wino_m=2)."""
+    boxes, topk). engine_kw: Engine options other than the product defaults (e.g. wino_m=2). model: a
+    drop-in model built elsewhere (e.g. through from_pretrained as the deployment builds it)."""
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
     from spotter_amd.config import PRESETS
     from spotter_amd.engine import Engine
 
     g = np.load(os.path.join(GOLD, f"{preset}_640.npz"))
-    model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False, precision=precision)
+    if model is None:
+        model = SpotterForObjectDetection(PRESETS[preset], use_graphs=False, precision=precision)
+    assert model.precision == precision
     if engine_kw:
         model._engine = Engine(model.cfg, model._host_weights(), torch.device("cuda", 0), precision=precision,
                                **engine_kw)
@@ -209,18 +212,30 @@ BF16_R101_P95_DSCORE = 0.04  # measured 0.012 (p50 0.004)
 BF16_R101_MAP = 0.90        # measured 0.958 (AP50 0.959)
 
 
-def test_r101vd_bf16_bs32_config_c4_replica():
+def test_r101vd_bf16_bs32_config_c4_replica(monkeypatch):
     """C4's per-replica workload: R101vd bf16 at batch 32 on one GPU (one Serve replica per MI355X;
-    serve.py:203, MODEL_NAME PekingU/rtdetr_v2_r101vd). The 4 r101vd goldens tiled ×8 through
-    Engine(precision="bf16") in one batch, at the stated bf16 bar against the HF fp32 goldens; every copy of
-    an image in the batch is bit-identical; a bs1 call of the same engine gives each image what the batch
-    gives, to the size of the bf16 delta itself (split-K at bs1 reorders the fp32 sums that feed bf16)."""
+    serve.py:203, MODEL_NAME PekingU/rtdetr_v2_r101vd). The model is built as the deployed drop-in builds it
+    (spotter_amd/dropin.py: from_pretrained with SPOTTER_PRECISION, here "bf16" as
+    deploy/rayservice-template.yaml sets it; MODEL_NAME synthetic:r101vd = the goldens' weights) and pickled
+    as Ray ships it to a replica. The 4 r101vd goldens tiled ×8 in one batch, at the stated bf16 bar against
+    the HF fp32 goldens; every copy of an image in the batch is bit-identical; a bs1 call of the same engine
+    gives each image what the batch gives, to the size of the bf16 delta itself (split-K at bs1 reorders
+    the fp32 sums that feed bf16)."""
+    import pickle
+
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from spotter_amd import SpotterImageProcessor
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.dropin import PRECISION_ARG
     from tools.bf16_delta import ap_vs_fp32, match_stats
     from types import SimpleNamespace
 
-    model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, "bf16")
+    monkeypatch.setenv("SPOTTER_PRECISION", "bf16")
+    built = eval(f"SpotterForObjectDetection.from_pretrained('synthetic:r101vd', {PRECISION_ARG})",
+                 {"SpotterForObjectDetection": SpotterForObjectDetection, "os": os})
+    replica = pickle.loads(pickle.dumps(built))  # AmenitiesDetector.bind ships the model pickled
+    replica.use_graphs = False
+    model, g, dets, logits, boxes, topk = run_tiled_batch("r101vd", 8, "bf16", model=replica)
+    assert model.engine.precision == "bf16" and model.engine._conv_mode == model.engine._lin_mode == "bf16"
     assert logits.shape == (32, 300, 80)
     proc = SpotterImageProcessor()
     st = match_stats(dets, g)

@@ -484,6 +484,9 @@ def test_rayservice_template_renders():
     # as the reference template (configs/rayservice-template.yaml:41-59): no pod overrides MODEL_NAME,
     # the image's ENV decides for head and workers alike
     assert "MODEL_NAME" not in env and "MODEL_NAME" not in {e["name"] for e in head.get("env", [])}
+    # C4 (BASELINE configs[3]): bf16 replicas, set where serve.py is imported (head: app build) and run (workers)
+    head_env = {e["name"]: e["value"] for e in head.get("env", [])}
+    assert env["SPOTTER_PRECISION"] == head_env["SPOTTER_PRECISION"] == "bf16"
 
 
 def _dockerfile_recipe():
@@ -597,7 +600,7 @@ def test_dropin_script_patches_serve_py(tmp_path):
         assert r.returncode == 0, r.stderr
     out = p.read_text()
     dropin.check(out)
-    assert out.count("SpotterForObjectDetection.from_pretrained(model_name)") == 1
+    assert out.count("SpotterForObjectDetection.from_pretrained(") == 1 and out.count(dropin.PRECISION_ARG) == 1
     assert out.count("Image = image_module()") == 1
     assert out.count("with Image.open(BytesIO(image_bytes)) as img_raw:") == src.count("with Image.open(")
     back = out

@@ -104,6 +104,29 @@ def test_unsupported_forms_raise():
         decode_coefs(data[:100])
 
 
+def _with_frame_size(data: bytes, w: int, h: int) -> bytes:
+    """The JPEG with its SOF0 header's height / width fields rewritten."""
+    i = data.index(b"\xff\xc0")
+    b = bytearray(data)
+    b[i + 5:i + 9] = bytes([h >> 8, h & 255, w >> 8, w & 255])
+    return bytes(b)
+
+
+@pytest.mark.parametrize("w,h", [(65501, 8), (8, 65501), (65535, 65535)])
+def test_frames_above_libjpegs_max_dimension_are_left_to_pillow(w, h):
+    """libjpeg's JPEG_MAX_DIMENSION (65500, jmorecfg.h): jdinput.c raises JERR_IMAGE_TOO_BIG above it, so the
+    strict parser refuses such frames at the header and the file goes to Pillow, which raises as
+    the reference does. 65500 itself passes the header check (this file then fails later: its data is 8×8)."""
+    from spotter_amd.jpeg import UnsupportedJpeg, decode_coefs
+
+    data = _jpeg(synthetic_image(4, 8, 8), quality=90)
+    with pytest.raises(UnsupportedJpeg, match="wider or higher than 65500"):
+        decode_coefs(_with_frame_size(data, w, h))
+    with pytest.raises((UnsupportedJpeg, RuntimeError)) as e:
+        decode_coefs(_with_frame_size(data, min(w, 65500), min(h, 65500)))
+    assert "wider or higher" not in str(e.value)
+
+
 def test_truncated_or_corrupt_data_is_left_to_pillow():
     """Entropy-coded data cut short, or a file without its EOI: Pillow raises ("image file is truncated")
     or applies its own LOAD_TRUNCATED_IMAGES policy, which is not libjpeg arithmetic — the decoder reports

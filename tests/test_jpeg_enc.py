@@ -95,8 +95,11 @@ def test_plan_refuses_what_it_does_not_encode():
 
     L = load()
     lay = SpJpegEncLayout()
-    for args in ((0, 10, -1, -1), (10, 70000, -1, -1), (10, 10, 0, -1), (10, 10, 101, -1), (10, 10, -1, 3)):
-        assert L.sp_jpeg_enc_plan(*args, C.byref(lay)) == -1, args
+    for args in ((0, 10, -1, -1), (10, 70000, -1, -1), (10, 10, 0, -1), (10, 10, 101, -1), (10, 10, -1, 3),
+                 (65501, 8, -1, -1), (8, 65501, -1, -1), (65535, 1, -1, -1)):
+        assert L.sp_jpeg_enc_plan(*args, C.byref(lay)) == -1, args  # 65501+: libjpeg's JERR_IMAGE_TOO_BIG
+    for args in ((65500, 8, -1, -1), (8, 65500, -1, -1)):  # JPEG_MAX_DIMENSION itself is encodable
+        assert L.sp_jpeg_enc_plan(*args, C.byref(lay)) == 0, args
 
 
 def test_which_saves_take_the_gpu_encoder():
@@ -115,3 +118,7 @@ def test_which_saves_take_the_gpu_encoder():
         assert _gpu_jpeg_options(im, buf, fmt, params) is None, (fmt, params)
     assert _gpu_jpeg_options(im, "out.jpg", "JPEG", {}) is None  # file names: Pillow's save
     assert _gpu_jpeg_options(Image.new("L", (8, 8)), buf, "JPEG", {}) is None
+    # above libjpeg's JPEG_MAX_DIMENSION Pillow's save raises JERR_IMAGE_TOO_BIG: that save stays Pillow's
+    assert _gpu_jpeg_options(Image.new("RGB", (65500, 1)), buf, "JPEG", {}) == (-1, -1, None)
+    for size in ((65501, 1), (1, 65501)):
+        assert _gpu_jpeg_options(Image.new("RGB", size), buf, "JPEG", {}) is None
