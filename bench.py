@@ -54,6 +54,8 @@ def parse():
                     help="batch of the CPU comparison leg (BASELINE.md §3: bs32; 0 = bs1 leg only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-events", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--no-input-supply", action="store_true",
+                    help="skip the host-input leg (pinned-host uint8 batches uploaded each step) and host decode rates")
     ap.add_argument("--latency-iters", type=int, default=100,
                     help="bs1 /detect core requests for the p50 latency half of the metric (0 = skip)")
     ap.add_argument("--detail", default=None, help="write per-conv-shape timings (JSON) here")
@@ -481,7 +483,96 @@ def make_step(args, rank, local):
         ops.postprocess(logits, pred, tsz, K, 0.5, scores, labels, boxes, counts, work)
 
     step.cfg, step.weights = cfg, weights
+    step.input_supply = None
+    if args.stream == "same":
+        step.input_supply = lambda steps, warmup: host_input_leg(torch, ops, eng, imgs_host, dev, px, batches[0][1],
+                                                                 (scores, labels, boxes, counts, work), S, K,
+                                                                 steps, warmup)
     return step, torch.cuda.synchronize, ops.set_launch_hook
+
+
+def host_input_leg(torch, ops, eng, imgs_host, dev, px, tsz, outs, S, K, steps, warmup):
+    """The same step with its uint8 batch supplied from pinned HOST memory every step (SURVEY §8e "Risks"):
+    a copy stream uploads batch i+1 into one of two device slots while the compute stream runs step i (the
+    upload waits only until step i-1's preprocess has read that slot). Returns (img/s, H2D facts)."""
+    import numpy as np
+
+    B = len(imgs_host)
+    pinned = torch.from_numpy(np.stack(imgs_host)).pin_memory()  # [B, S, S, 3] uint8
+    slots = [torch.empty(pinned.shape, dtype=torch.uint8, device=dev) for _ in range(2)]
+    copy_s, comp = torch.cuda.Stream(dev), torch.cuda.current_stream(dev)
+    uploaded = [torch.cuda.Event() for _ in range(2)]
+    read = [torch.cuda.Event() for _ in range(2)]
+
+    def upload(i):
+        k = i % 2
+        copy_s.wait_event(read[k])  # step i-2's preprocess has consumed this slot
+        with torch.cuda.stream(copy_s):
+            slots[k].copy_(pinned, non_blocking=True)
+        uploaded[k].record(copy_s)
+
+    def run(n):
+        upload(0)
+        for i in range(n):
+            if i + 1 < n:
+                upload(i + 1)
+            k = i % 2
+            comp.wait_event(uploaded[k])
+            ops.preprocess_u8([slots[k][b] for b in range(B)], px, S, S)
+            read[k].record(comp)
+            logits, pred = eng.forward(px)
+            ops.postprocess(logits, pred, tsz, K, 0.5, *outs)
+
+    run(max(2, warmup))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter() - t0
+    # the upload alone, back to back on the copy stream
+    n_up = 10
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(copy_s)
+    with torch.cuda.stream(copy_s):
+        for _ in range(n_up):
+            slots[0].copy_(pinned, non_blocking=True)
+    e1.record(copy_s)
+    torch.cuda.synchronize(dev)
+    up_ms = e0.elapsed_time(e1) / n_up
+    nbytes = pinned.numel()
+    return B * steps / t, {"bytes_per_batch": nbytes, "h2d_ms_per_batch": round(up_ms, 3),
+                           "h2d_gbps": round(nbytes / up_ms / 1e6, 1), "ms_per_step": round(1000 * t / steps, 3)}
+
+
+def host_decode_rates(seconds=1.0):
+    """Host JPEG entropy decode per core (the Huffman half of the drop-in's GPU decode, sp_jpeg_decode_coefs, one
+    thread) and Pillow's whole decode (what the reference runs, serve.py:96-97), images/s per core, for the
+    reference's 1200x717 fixture and a 640x640 JPEG of the bench's synthetic content (Pillow quality 75)."""
+    import io
+
+    from PIL import Image
+
+    from spotter_amd.jpeg import decode_coefs
+    from spotter_amd.synthetic import synthetic_batch
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, "tests", "golden", "test_pic.jpg"), "rb") as f:
+        fixture = f.read()
+    b = io.BytesIO()
+    Image.fromarray(synthetic_batch(1, 640, 640, seed0=1234)[0]).save(b, "JPEG", quality=75)
+    out = {}
+    for name, data in (("fixture_1200x717", fixture), ("synthetic_640x640_q75", b.getvalue())):
+        rates = {}
+        for what, fn in (("entropy_decode", lambda d=data: decode_coefs(d)),
+                         ("pillow_decode", lambda d=data: Image.open(io.BytesIO(d)).convert("RGB"))):
+            fn()
+            n, t0 = 0, time.perf_counter()
+            while time.perf_counter() - t0 < seconds:
+                fn()
+                n += 1
+            rates[what] = round(n / (time.perf_counter() - t0), 1)
+        out[name] = {"bytes": len(data), "img_per_s_per_core": rates}
+    return out
 
 
 def main():
@@ -613,6 +704,25 @@ def main():
             cpu = {"value": None, "unit": "images/sec", "cores": None, "kind": "reference",
                    "sample": f"unavailable: {type(e).__name__}: {e}"}
 
+    supply = None
+    if (rank == 0 and world == 1 and not args.no_input_supply and args.stub_step_ms is None
+            and getattr(step, "input_supply", None) is not None):
+        try:
+            v_host, h2d = step.input_supply(args.steps, args.warmup)
+            dec = host_decode_rates()
+            per_core = dec["synthetic_640x640_q75"]["img_per_s_per_core"]["entropy_decode"]
+            supply = {"host_input_img_s": round(v_host, 2), "resident_img_s": round(value, 2),
+                      "host_vs_resident": round(v_host / value, 4), **h2d,
+                      "pcie_bound_img_s": round(B / (h2d["h2d_ms_per_batch"] / 1e3), 1),
+                      "host_decode": dec,
+                      "host_cores_per_gpu_at_resident_rate": round(value / per_core, 1),
+                      "note": "host_input: the bs32 uint8 batch uploaded from pinned host memory each step on a copy "
+                              "stream overlapping the previous step's compute; host_decode: one core, images/s; "
+                              "cores per GPU = resident img/s / the 640x640 entropy-decode rate (the GPU does the "
+                              "rest of the decode)"}
+        except Exception as e:
+            supply = {"error": f"{type(e).__name__}: {e}"}
+
     lat = None
     if rank == 0 and world == 1 and args.latency_iters > 0 and args.stub_step_ms is None:
         try:
@@ -655,6 +765,7 @@ def main():
                        "parallelism": f"replicas x{world}"},
             "per_rank": per_rank,
             "roofline": roof, "kernel_classes": classes, "cpu_baseline": cpu, "latency": lat,
+            "input_supply": supply,
         }
         # vs_baseline stays null: BASELINE.md §1 holds no published number for this metric (the reference
         # publishes none). The same-run CPU reference ratio is reported beside it.

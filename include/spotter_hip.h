@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 13
+#define SP_ABI_VERSION 14
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -140,6 +140,14 @@ typedef struct {
 
 int sp_abi_version(void);
 const char* sp_last_error(void);
+/* ABI v14: what this library was compiled with (no device call). SP_BUILD_FUSED_LN: the fused-LayerNorm
+ * GEMM epilogue (sp_conv_desc.ln_gamma; diagnostic builds only); SP_BUILD_BOUNDS: the bounds-check build. */
+enum sp_build_flag { SP_BUILD_FUSED_LN = 1, SP_BUILD_BOUNDS = 2 };
+int sp_build_flags(void);
+/* ABI v14, bounds-check builds (SP_BUILD_BOUNDS): synchronises the device, returns the number of index
+ * violations the kernels recorded since the last call (and resets the counts), and writes one line per
+ * offending source unit ("file:line hits=… index=… extent=…") into buf. -1 on a product build. */
+int64_t sp_bounds_report(char* buf, int64_t cap);
 int sp_device_init(int device);
 /* Frees the cached resample coefficient tables (the only state kept across
  * calls). Safe to call at any time; the next sp_preprocess_u8 rebuilds what it needs. */

@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -82,9 +82,13 @@ class SpJpegEncLayout(C.Structure):
 
 
 SP_JPEG_UNSUPPORTED = -10
+SP_BUILD_FUSED_LN = 1  # sp_build_flags bits (include/spotter_hip.h)
+SP_BUILD_BOUNDS = 2
 
 _SIGS = {
     "sp_abi_version": (i32, []),
+    "sp_build_flags": (i32, []),
+    "sp_bounds_report": (i64, [C.c_char_p, i64]),
     "sp_last_error": (C.c_char_p, []),
     "sp_device_init": (i32, [i32]),
     "sp_shutdown": (i32, []),

@@ -1,10 +1,14 @@
 """Builds libspotter_hip.so in-tree with hipcc for gfx950 (MI355X).
 
-    python -m spotter_amd.build_ext [--force]
+    python -m spotter_amd.build_ext [--force] [--bounds]
 
 Objects go to spotter_amd/_build/, the library to spotter_amd/libspotter_hip.so
 (git-ignored; it travels to the GPU box with the gpurun snapshot). Sources are
 compiled in parallel and only when newer than their object.
+
+--bounds: the bounds-check diagnostic library instead (every unit with -DSP_BOUNDS=1; objects in
+spotter_amd/_build_bounds/, library spotter_amd/_bounds/libspotter_bounds.so; select it with
+SPOTTER_HIP_LIB). Its kernels count index violations (SP_BCHECK, csrc/common.h) for sp_bounds_report.
 """
 from __future__ import annotations
 
@@ -53,32 +57,38 @@ def _deps_mtime(src: str):
     return max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _includes(src, set())])
 
 
-def _compile(src: str, force: bool) -> str:
-    obj = os.path.join(BUILD, os.path.basename(src).replace(".hip", ".o"))
+BOUNDS_BUILD = os.path.join(HERE, "_build_bounds")
+BOUNDS_LIB = os.path.join(HERE, "_bounds", "libspotter_bounds.so")
+
+
+def _compile(src: str, force: bool, build_dir: str = BUILD, extra=()) -> str:
+    obj = os.path.join(build_dir, os.path.basename(src).replace(".hip", ".o"))
     if not force and os.path.exists(obj):
         if os.path.getmtime(obj) >= _deps_mtime(src):
             return obj
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *extra, "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, verbose: bool = True, bounds: bool = False) -> str:
+    build_dir, lib, extra = (BOUNDS_BUILD, BOUNDS_LIB, ("-DSP_BOUNDS=1",)) if bounds else (BUILD, LIB, ())
+    os.makedirs(build_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        objs = list(ex.map(lambda s: _compile(s, force, build_dir, extra), srcs))
+    if force or not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", lib]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr}")
         if verbose:
-            print(f"built {LIB}")
-    return LIB
+            print(f"built {lib}")
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, bounds="--bounds" in sys.argv)

@@ -28,6 +28,8 @@
 #define SP_DIAG_KERNELS 0
 #endif
 
+bool sp::conv_gemm_has_fused_ln() { return SP_DIAG_KERNELS != 0; }
+
 namespace sp {
 
 namespace {

@@ -53,6 +53,9 @@ __global__ __launch_bounds__(256) void msda_kernel(const sp_msda_desc d) {
       const bool vx0 = xi0 >= 0 && xi0 < W, vx1 = xi0 + 1 >= 0 && xi0 + 1 < W;
       const bool vy0 = yi0 >= 0 && yi0 < H, vy1 = yi0 + 1 >= 0 && yi0 + 1 < H;
       float s = 0.f;
+      // corner rows of this image's level l: [level_start[l], level_start[l] + H·W) of the B·S value rows
+      if (vy0 && vx0) SP_BCHECK((int64_t)b * d.S + d.level_start[l] + (int64_t)yi0 * W + xi0, (int64_t)d.B * d.S);
+      if (vy1 && vx1) SP_BCHECK((int64_t)b * d.S + d.level_start[l] + (int64_t)(yi0 + 1) * W + xi0 + 1, (int64_t)d.B * d.S);
       if (vy0 && vx0) s += vl[((int64_t)yi0 * W + xi0) * d.ld_value] * wnw;
       if (vy0 && vx1) s += vl[((int64_t)yi0 * W + xi0 + 1) * d.ld_value] * wne;
       if (vy1 && vx0) s += vl[((int64_t)(yi0 + 1) * W + xi0) * d.ld_value] * wsw;
@@ -60,6 +63,7 @@ __global__ __launch_bounds__(256) void msda_kernel(const sp_msda_desc d) {
       out += s * a;
     }
   }
+  SP_BCHECK(h * d.head_dim + c, d.ld_out);
   d.out[row * d.ld_out + h * d.head_dim + c] = out;
 }
 
@@ -104,6 +108,8 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, con
   for (int i = 0; i < LP; ++i) den += expf(logit[i] - mx);
   const float nps = 1.0f / (float)d.points;
   const VT* vbase = value + (int64_t)b * d.S * d.ld_value + d.value_col + h * d.head_dim + c;
+  SP_BCHECK(d.value_col + h * d.head_dim + c + 3, d.ld_value);
+  SP_BCHECK(h, d.heads);
   float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int l = 0; l < d.levels; ++l) {
     const int H = d.level_h[l], W = d.level_w[l];
@@ -131,6 +137,10 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, con
       const bool vy0 = yi0 >= 0 && yi0 < H, vy1 = yi0 + 1 >= 0 && yi0 + 1 < H;
       const int cx0 = min(max(xi0, 0), W - 1), cx1 = min(max(xi0 + 1, 0), W - 1);
       const int cy0 = min(max(yi0, 0), H - 1), cy1 = min(max(yi0 + 1, 0), H - 1);
+      // the clamped corners stay inside level l of image b (value rows [b·S, (b+1)·S)), channels inside the row
+      SP_BCHECK((int64_t)b * d.S + d.level_start[l] + (int64_t)cy0 * W + cx0, (int64_t)d.B * d.S);
+      SP_BCHECK((int64_t)b * d.S + d.level_start[l] + (int64_t)cy1 * W + cx1, (int64_t)d.B * d.S);
+      SP_BCHECK(d.level_start[l] + (int64_t)cy1 * W + cx1, d.level_start[l] + (int64_t)H * W);
       const float4 vnw = corner4(vl + ((int64_t)cy0 * W + cx0) * d.ld_value);
       const float4 vne = corner4(vl + ((int64_t)cy0 * W + cx1) * d.ld_value);
       const float4 vsw = corner4(vl + ((int64_t)cy1 * W + cx0) * d.ld_value);
@@ -148,6 +158,7 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, con
       out.x += s.x * a; out.y += s.y * a; out.z += s.z * a; out.w += s.w * a;
     }
   }
+  SP_BCHECK(h * d.head_dim + c + 3, d.ld_out);
   *reinterpret_cast<float4*>(d.out + row * d.ld_out + h * d.head_dim + c) = out;
 }
 

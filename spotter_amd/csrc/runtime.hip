@@ -18,6 +18,61 @@ void clear_error() { g_err[0] = 0; }
 
 extern "C" int sp_abi_version(void) { return SP_ABI_VERSION; }
 
+namespace sp {
+namespace {
+struct BoundsUnit {
+  const char* unit;
+  int (*read)(BoundsLog*, int);
+};
+// function-local storage: the registrations run from other units' static initialisers
+BoundsUnit* bounds_units(int** count) {
+  static BoundsUnit units[64];
+  static int n = 0;
+  *count = &n;
+  return units;
+}
+}  // namespace
+
+int bounds_register(const char* unit, int (*read)(BoundsLog*, int)) {
+  int* n;
+  BoundsUnit* u = bounds_units(&n);
+  if (*n < 64) u[(*n)++] = {unit, read};
+  return *n;
+}
+}  // namespace sp
+
+extern "C" int sp_build_flags(void) {
+  return (sp::conv_gemm_has_fused_ln() ? SP_BUILD_FUSED_LN : 0) | (SP_BOUNDS ? SP_BUILD_BOUNDS : 0);
+}
+
+extern "C" int64_t sp_bounds_report(char* buf, int64_t cap) {
+#if SP_BOUNDS
+  int* n;
+  sp::BoundsUnit* u = sp::bounds_units(&n);
+  int64_t total = 0, used = 0;
+  if (buf && cap > 0) buf[0] = 0;
+  for (int i = 0; i < *n; ++i) {
+    sp::BoundsLog lg;
+    if (u[i].read(&lg, 1) != 0) {
+      sp::set_error("sp_bounds_report: reading the log of %s failed", u[i].unit);
+      return -2;
+    }
+    total += lg.hits;
+    if (lg.hits && buf && used < cap) {
+      const int w = snprintf(buf + used, (size_t)(cap - used), "%s:%d hits=%u index=%lld extent=%lld\n",
+                             u[i].unit, lg.line, lg.hits, lg.index, lg.extent);
+      if (w > 0) used += w;
+    }
+  }
+  return total;
+#else
+  (void)buf;
+  (void)cap;
+  sp::set_error("sp_bounds_report: not a bounds-check build (python -m spotter_amd.build_ext --bounds)");
+  return -1;
+#endif
+}
+
 extern "C" const char* sp_last_error(void) { return sp::g_err; }
 
 namespace sp {

@@ -149,7 +149,7 @@ class Engine:
                  fuse_ln: bool = False, winograd: str | bool = "auto", wino_m: int = 4,
                  bf16_store: bool | None = None, direct_c32: bool = True,
                  direct_c64_bf16: bool = True, splitk_combine: bool = False):
-        from ._lib import lib
+        from ._lib import SP_BUILD_FUSED_LN, lib
 
         check_precision(precision)
         self.cfg = cfg
@@ -163,6 +163,10 @@ class Engine:
         if fuse_ln and PRECISIONS.get(precision, ("", ""))[1] == "bf16":
             # the fused-LN tile runs fp32 weights: it would silently raise the bf16 linears' operand precision
             raise ValueError(f"fuse_ln=True runs the linears on fp32 weights: not available with precision={precision!r}")
+        if fuse_ln and not (lib().sp_build_flags() & SP_BUILD_FUSED_LN):
+            # refuse here, not at the first fused GEMM in the middle of a forward
+            raise ValueError("fuse_ln=True needs a diagnostic library with the fused-LayerNorm tiles "
+                             "(UNIT=conv_gemm tools/build_diag.sh <name> -DSP_DIAG_KERNELS=1; SPOTTER_HIP_LIB)")
         # stride-1 3x3 convs as Winograd F(m x m, 3x3) on the split GEMM (sp_winograd_f{2,4}3_*): "auto"
         # (default) = those on the split operand mode with Cin >= 128 for F(4x4) (1.4-2.6x faster than the
         # implicit GEMM at bs32, profiles/r2/tune_wino_f43_x3.json) or Cin >= 256 for F(2x2) (1.25-1.8x,
@@ -462,7 +466,9 @@ class Engine:
         40²x384 / 80²x128 convs measured 2.6x / 1.45x / 1.09x, 40²x256 1.04x, 20²x384 / 20²x512 0.85-0.95x
         (profiles/r2/tune_wino_f43_bs1.json); every bs8 / bs32 map clears it."""
         if self.wino_m == 4:
-            return pixels * cin >= self.WINO43_MIN_WORK and cin >= self.WINO43_MIN_CIN
+            # the Cin gate belongs to the "auto" policy only (as in _add_wino): a forced winograd=True / "all"
+            # has built the transformed weights for the thin convs too and runs them
+            return pixels * cin >= self.WINO43_MIN_WORK and (cin >= self.WINO43_MIN_CIN or self.winograd != "auto")
         return pixels >= self.WINO_MIN_PIXELS
 
     def _cv(self, x: V, n, h, w, cw: ConvW, stride, out: V, act=None, res1=None, res2=None, **kw):

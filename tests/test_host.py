@@ -837,6 +837,27 @@ def test_engine_refuses_fused_layernorm_on_bf16_linears():
             Engine(PRESETS["r18vd"], {}, "cpu", precision=prec, fuse_ln=True)
 
 
+def test_product_library_build_flags():
+    """The product library has neither the fused-LayerNorm tiles nor bounds checks (sp_build_flags, no device
+    call): Engine(fuse_ln=True) is refused at construction, and sp_bounds_report says it is not a
+    bounds-check build."""
+    import ctypes
+
+    from spotter_amd._lib import LIB_PATH, load
+    from spotter_amd.build_ext import LIB
+    from spotter_amd.config import PRESETS
+    from spotter_amd.engine import Engine
+
+    if LIB_PATH != LIB:
+        pytest.skip("SPOTTER_HIP_LIB selects another library")
+    L = load()
+    assert L.sp_build_flags() == 0
+    buf = ctypes.create_string_buffer(256)
+    assert L.sp_bounds_report(buf, 256) == -1 and b"not a bounds-check build" in L.sp_last_error()
+    with pytest.raises(ValueError, match="diagnostic library"):
+        Engine(PRESETS["r18vd"], {}, "cpu", precision="fp32", fuse_ln=True)
+
+
 def test_merge_tile_table_keeps_entries_and_skips_winograd(tmp_path):
     """tools/merge_tile_table.py (round 4): a measured winner beyond --min-gain replaces or adds its (shape,
     mode) entry, a "-" win or a small gain leaves the table as it was, the Winograd component GEMMs of a

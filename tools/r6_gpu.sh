@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-6 GPU passes (GPU box, repo root):
+#   tools/r6_gpu.sh serve <tag>   GPU suite, the k-replicas-per-GPU whole-request sweep (fp32, bf16), the bench's
+#                                 default line with its input-supply leg, the MSDA gather ceiling, x3 stage-3 PMC
+set -euo pipefail
+PART=$1
+OUT=gpurun_out/${2:-r6}; mkdir -p $OUT; export TMPDIR=/tmp
+if [ "$PART" = serve ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+  tail -1 $OUT/gpu_tests.log
+  timeout -k 10 600 python3 -u tools/served_sweep.py --k 1 2 4 --precision fp32 bf16 --seconds 8 --out $OUT/served > $OUT/served.log 2>&1
+  cat $OUT/served.log | cut -c1-240
+  timeout -k 10 300 python3 -u tools/microbench/gather_ceiling.py --out $OUT/gather_ceiling.json > $OUT/gather.log 2>&1
+  tail -1 $OUT/gather.log | cut -c1-400
+  timeout -k 10 600 python3 -u bench.py > $OUT/bench.log 2>&1
+  tail -1 $OUT/bench.log | cut -c1-200
+  bash tools/pmc.sh $OUT/pmc_x3 --prec f32x3 --shapes 3,4 > $OUT/pmc_x3.log 2>&1
+  tail -5 $OUT/pmc_x3.log
+  echo r6 serve done
+fi
