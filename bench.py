@@ -190,9 +190,10 @@ class KernelEventRecorder:
         for k, e0, e1, f, nb, shp in self.recs:
             c = out.setdefault(k, {"ms": 0.0, "ivs": [], "flops": 0, "bytes": 0, "n": 0, "gather": 0})
             if k == "msda" and shp:
-                # bytes the bilinear taps fetch (4 corners × Dh fp32 per sample), L2-served: SURVEY §8 D1.4
-                B_, S_, Q_, H_, Dh_, L_, P_ = shp
-                c["gather"] += B_ * Q_ * H_ * L_ * P_ * 4 * Dh_ * 4
+                # bytes the bilinear taps fetch (4 corners × Dh value elements per sample), L2-served: SURVEY §8 D1.4
+                B_, S_, Q_, H_, Dh_, L_, P_ = shp[:7]
+                esz = shp[7] if len(shp) > 7 else 4  # value-row element size (bf16 rows: 2)
+                c["gather"] += B_ * Q_ * H_ * L_ * P_ * 4 * Dh_ * esz
             a, b = self.t0.elapsed_time(e0), self.t0.elapsed_time(e1)
             c["ms"] += b - a
             c["ivs"].append((a, b))
@@ -220,6 +221,28 @@ def load_traffic(args, avg_alg_bytes, key="conv"):
     b = e["hbm_bytes_per_launch"]
     return b, {"source": f"profiles/pmc_traffic.json[{cfg_key}].classes.{key}",
                "ratio_to_algorithmic": round(b / avg_alg_bytes, 3)}
+
+
+def load_gather_ceiling(args, dec_layers):
+    """The measured random row-segment gather ceiling for this config's MSDA address pattern
+    (tools/microbench/gather_ceiling.py → profiles/r6/msda/gather_ceiling.json): the case with this value-row
+    dtype, level maps and batch, preferring this value_all row length. (GB/s, case) or (None, None)."""
+    path = os.path.join(ROOT, "profiles", "r6", "msda", "gather_ceiling.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        cases = json.load(f)["cases"]
+    s = args.size // 640
+    dt = "bf16" if args.precision in ("bf16", "bf16-all") else "fp32"
+    want_map = f"{80 * s}^2+{40 * s}^2+{20 * s}^2"
+    ok = [c for c in cases if c["dtype"] == dt and c["map"] == want_map and c["B"] == args.batch]
+    if not ok:
+        return None, None
+    ld = dec_layers * 256
+    exact = [c for c in ok if c["ld"] == ld]
+    best = max(exact or ok, key=lambda c: c["gather_gbps"])
+    return best["gather_gbps"], {"source": "profiles/r6/msda/gather_ceiling.json",
+                                 "case": f"{dt} {want_map} B{args.batch} ld{best['ld']} npt{best['npt']}"}
 
 
 def cpu_baseline(cfg, weights, seconds, batch):
@@ -682,11 +705,19 @@ def main():
                 else:
                     classes[kind]["bytes_basis"] = "whole_value_map (no PMC traffic for this config)"
             if c.get("gather"):
+                g_rate = c["gather"] / 1e9 / (c["busy"] * 1e-3)
                 classes[kind]["l2_gather"] = {
-                    "achieved": round(c["gather"] / 1e9 / (c["busy"] * 1e-3), 1), "unit": "GB/s",
+                    "achieved": round(g_rate, 1), "unit": "GB/s",
                     "bytes_per_launch": c["gather"] // c["n"],
-                    "note": "sampled-corner bytes (4 taps × Dh × 4 B per sample); the value map stays in L2 / "
-                            "Infinity Cache, so this is an L2 gather rate, not an HBM bound"}
+                    "note": "sampled-corner bytes (4 taps × Dh × element size per sample); the value map stays in "
+                            "L2 / Infinity Cache, so this is an L2 gather rate, not an HBM bound"}
+                gc, gnote = load_gather_ceiling(args, step.cfg.decoder_layers)
+                if gc:
+                    classes[kind]["gather_ceiling"] = {
+                        "peak": gc, "unit": "GB/s", "frac": round(g_rate / gc, 4), **gnote,
+                        "note": "measured ceiling of random 128-byte (fp32) / 64-byte (bf16) row-segment gathers in "
+                                "msda's address pattern on this chip (uniform random locations, XCD-major grid); "
+                                "frac = l2_gather.achieved / peak"}
         roof = conv_roofline(rec, cl, args, bf, rec_timed)
         roof["events"] = ("timed region: events around the dominant kernel's launches of one sampled step "
                           "(step K//2); kernel_classes, modes and conv_class: a separate untimed pass of the "

@@ -171,6 +171,7 @@ int sp_set_splitk_config(int cfg, int max_splits, int min_ktiles);
  * A/B measurements; nothing on the product path calls it. */
 enum sp_tuning_knob {
   SP_TUNE_GLDS_EPILOGUE = 3,  /* split-mode slab epilogue: 4 = outputs stored from the accumulators, else the slab pass */
+  SP_TUNE_MSDA_GENERIC = 4,   /* ABI v14: 1 = sp_msda's per-lane kernel where the point-sharing one applies (A/B) */
 };
 int sp_set_tuning(int knob, int value);
 

@@ -60,6 +60,11 @@ __global__ __launch_bounds__(256) void attn_mfma_kernel(const float* __restrict_
   int qtile, hh, b;
   attn_work(n, heads, qtile, hh, b);
   const int64_t rowbase = (int64_t)b * n;
+  // this head's channels lie inside every operand row (q / k / v may be slices of one fused projection)
+  SP_BCHECK(hh * DH + DH - 1, ldq);
+  SP_BCHECK(hh * DH + DH - 1, ldk);
+  SP_BCHECK(hh * DH + DH - 1, ldv);
+  SP_BCHECK(hh * DH + DH - 1, ldo);
   const int q0 = qtile * 64 + wave * 16;
   const int qi = q0 + c16;
   // B operand of Sᵀ = K Qᵀ: step s, lane group g supplies channel g·QS + s of query qi.
@@ -179,6 +184,11 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(const float* __restrict_
   int qtile, hh, b;
   attn_work(n, heads, qtile, hh, b);
   const int64_t rowbase = (int64_t)b * n;
+  // this head's channels lie inside every operand row (q / k / v may be slices of one fused projection)
+  SP_BCHECK(hh * DH + DH - 1, ldq);
+  SP_BCHECK(hh * DH + DH - 1, ldk);
+  SP_BCHECK(hh * DH + DH - 1, ldv);
+  SP_BCHECK(hh * DH + DH - 1, ldo);
   const int qi = qtile * 64 + wave * 16 + c16;
   bf16x4_s qv[QC];  // channels 16c + 4g .. +3 of query qi
   {

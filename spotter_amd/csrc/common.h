@@ -67,6 +67,9 @@ struct BoundsLog {
 int bounds_register(const char* unit, int (*read)(BoundsLog* out, int reset));
 // what the library was compiled with (sp_build_flags): conv_gemm.hip's fused-LayerNorm tiles
 bool conv_gemm_has_fused_ln();
+// msda.hip's tuning hook (sp_set_tuning SP_TUNE_MSDA_GENERIC)
+int msda_generic();
+void set_msda_generic(int v);
 
 #if SP_BOUNDS
 namespace {

@@ -117,6 +117,8 @@ __device__ __forceinline__ void epilogue_vec(const ConvArgs& p, int64_t m, int n
 template <bool BF = false>
 __device__ __forceinline__ void epilogue_store(const ConvArgs& p, int64_t m, int n, float4 v) {
   const sp_conv_desc& d = p.d;
+  SP_BCHECK(m, p.M);
+  SP_BCHECK(n, d.Cout);
   if (p.vec_epi && n + 3 < d.Cout) {
     epilogue_vec<BF>(p, m, n, v, load_res1<BF>(d, m, n));
   } else {
@@ -155,6 +157,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t partial_rsrc(const ConvArgs& p
 template <bool CNT = false>
 __device__ __forceinline__ void store_partial(const ConvArgs& p, int64_t m, int n, float4 v) {
   const int64_t e = ((int64_t)blockIdx.z * p.M + m) * p.ldp + n;
+  SP_BCHECK(e + 3, p.d.workspace_elems);  // the split-K slabs [splits][M][ldp] fit the caller's workspace
+  SP_BCHECK(m, p.M);
   if (CNT && p.counters)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), partial_rsrc(p), (int)(e * 4), 0, 16);
   else

@@ -102,6 +102,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (a_ok[i] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W) {
           const int64_t pix = (int64_t)(a_base[i] + iy) * d.W + ix;
+          SP_BCHECK(pix, (int64_t)d.N * d.H * d.W);
+          SP_BCHECK(c0 + 3, d.Cin);
           v = *reinterpret_cast<const float4*>(d.A + pix * d.lda + c0);
           if (d.A2) {
             float4 w = *reinterpret_cast<const float4*>(d.A2 + pix * d.lda2 + c0);
@@ -114,6 +116,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(const ConvArgs p) {
       for (int i = 0; i < PB; ++i) {
         const int n = n0 + i * 32 + lrow;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < d.Cout) SP_BCHECK(k0 + lchunk * 4 + 3, p.K);
         if (n < d.Cout) v = *reinterpret_cast<const float4*>(d.Wt + (int64_t)n * p.K + k0 + lchunk * 4);
         rb[i] = v;
       }
@@ -259,6 +262,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const ConvArgs p) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = i / n4;
     const int n = (int)(i - m * n4) * 4;
+    SP_BCHECK(((int64_t)(p.splits - 1) * p.M + m) * p.ldp + n + 3, p.d.workspace_elems);
     float4 v = *reinterpret_cast<const float4*>(p.partial + m * p.ldp + n);
     for (int z = 1; z < p.splits; ++z) {
       float4 u = *reinterpret_cast<const float4*>(p.partial + ((int64_t)z * p.M + m) * p.ldp + n);
@@ -469,6 +473,9 @@ extern "C" int sp_set_tuning(int knob, int value) {
   switch (knob) {
     case SP_TUNE_GLDS_EPILOGUE:
       sp::set_glds_epilogue(value == 4 ? 4 : -1);
+      return 0;
+    case SP_TUNE_MSDA_GENERIC:
+      sp::set_msda_generic(value == 1 ? 1 : 0);
       return 0;
     default:
       sp::set_error("sp_set_tuning: unknown knob %d", knob);

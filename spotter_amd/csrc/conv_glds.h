@@ -100,6 +100,12 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
   const int mt = wg / tilesN;
   const int n0 = (wg - mt * tilesN) * BN;
   const int64_t m0 = (int64_t)mt * BM;
+  // the grid matches the problem: every tile starts inside M × Cout, k-tiles inside K, batch member inside batch
+  SP_BCHECK(m0, p.M);
+  SP_BCHECK(n0, d.Cout);
+  SP_BCHECK(bi, p.batch);
+  SP_BCHECK((int64_t)kt1 * BK - 1, p.K);
+  SP_BCHECK(kt0, kt1);
 
   // B pieces: row (j·NT + tid) / RB, global chunk (tid % RB) ^ swzB(row): (row >> 2) & 3 at BK = 32
   // (sw16), (row >> 3) & 1 at BK = 16.
@@ -127,6 +133,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     const int rem = (int)(mm - (int64_t)b * p.HoWo);
     const int oy = rem / d.Wo;
     const int ox = rem - oy * d.Wo;
+    SP_BCHECK(b, d.N);
     a_iy0[j] = ok ? oy * d.stride - d.pad : -(1 << 20);
     a_ix0[j] = ox * d.stride - d.pad;
     a_ptr[j] = A + (((int64_t)b * d.H + a_iy0[j]) * d.W + a_ix0[j]) * d.lda * ES + ca * 16;
@@ -147,6 +154,8 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
     for (int j = 0; j < GAP; ++j) {
       const int64_t m = m0 + (j * NT + tid) / RA;
       a_off[j] = (uint32_t)((m < p.M ? m : p.M - 1) * d.lda * ES + ca * 16);
+      SP_BCHECK((m < p.M ? m : p.M - 1) * d.lda + (ca + 1) * (16 / ES) - 1 + (int64_t)(kt1 - 1) * BK,
+                (p.M - 1) * d.lda + d.Cin);
     }
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
@@ -186,6 +195,9 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
       return;
     }
     const int64_t off = (((int64_t)s_kh * d.W + s_kw) * d.lda + s_c0) * ES;
+    // the tap walk stays inside the filter and each A piece's channels inside Cin (≤ lda)
+    SP_BCHECK(s_kh, d.KH);
+    SP_BCHECK(s_c0 + (ca + 1) * (16 / ES) - 1, d.Cin);
 #pragma unroll
     for (int j = 0; j < GAP; ++j) {
       const bool ok = (unsigned)(a_iy0[j] + s_kh) < (unsigned)d.H && (unsigned)(a_ix0[j] + s_kw) < (unsigned)d.W;
@@ -197,6 +209,7 @@ __device__ __forceinline__ void glds_main(const ConvArgs& p, uint4* smem, int wg
       }
     }
     const int k0 = kt * BK;
+    SP_BCHECK(k0 + cbk * 8 + 7, p.K);
 #pragma unroll
     for (int pl = 0; pl < PL; ++pl)
 #pragma unroll

@@ -40,6 +40,7 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const float4* __restric
     float4 m = ninf;
     if ((unsigned)iy >= (unsigned)h) return m;
     const float4* xr = x + ((int64_t)b * h + iy) * w * c4 + cc;
+    SP_BCHECK((int64_t)b * h + iy, (int64_t)n * h);
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
       const int ix = ox * 2 - 1 + dx;
@@ -58,6 +59,7 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const float4* __restric
       float4 m;
       m.x = fmaxf(fmaxf(prev.x, r0.x), r1.x); m.y = fmaxf(fmaxf(prev.y, r0.y), r1.y);
       m.z = fmaxf(fmaxf(prev.z, r0.z), r1.z); m.w = fmaxf(fmaxf(prev.w, r0.w), r1.w);
+      SP_BCHECK(((int64_t)b * ho + oy) * wo + ox, (int64_t)n * ho * wo);
       y[(((int64_t)b * ho + oy) * wo + ox) * ldy4 + cc] = m;
       prev = r1;
     }
@@ -79,6 +81,7 @@ __global__ __launch_bounds__(256) void avgpool2_kernel(const float4* __restrict_
       const int iy = oy * 2 + dy;
       if (iy >= h) continue;
       const float4* xr = x + ((int64_t)b * h + iy) * w * c4 + cc;
+      SP_BCHECK((int64_t)b * h + iy, (int64_t)n * h);
 #pragma unroll
       for (int dx = 0; dx < 2; ++dx) {
         const int ix = ox * 2 + dx;
@@ -125,6 +128,7 @@ __global__ __launch_bounds__(256) void maxpool3s2_bf16_kernel(const uint4* __res
     for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
     if ((unsigned)iy >= (unsigned)h) return;
     const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
+    SP_BCHECK((int64_t)b * h + iy, (int64_t)n * h);
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
       const int ix = ox * 2 - 1 + dx;
@@ -171,6 +175,7 @@ __global__ __launch_bounds__(256) void avgpool2_bf16_kernel(const uint4* __restr
       const int iy = oy * 2 + dy;
       if (iy >= h) continue;
       const uint4* xr = x + ((int64_t)b * h + iy) * w * c8 + cc;
+      SP_BCHECK((int64_t)b * h + iy, (int64_t)n * h);
 #pragma unroll
       for (int dx = 0; dx < 2; ++dx) {
         const int ix = ox * 2 + dx;
@@ -201,6 +206,8 @@ __global__ __launch_bounds__(256) void upsample2_kernel(const float4* __restrict
   const int wo = 2 * w;
   for (int row = blockIdx.y; row < n * h; row += gridDim.y) {  // row = b * h + iy
     const int b = row / h, iy = row - b * h;
+    SP_BCHECK(row, (int64_t)n * h);
+    SP_BCHECK(((int64_t)b * 2 * h + 2 * iy + 1) * wo + 2 * ix + 1, (int64_t)n * 4 * h * w);
     const float4 v = x[((int64_t)row * w + ix) * ldx4 + cc];
     float4* y0 = y + (((int64_t)b * 2 * h + 2 * iy) * wo + 2 * ix) * ldy4 + cc;
     float4* y1 = y0 + (int64_t)wo * ldy4;
@@ -353,6 +360,7 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src
     int c = (int)(i % d);
     int64_t r = i / d;  // b*k + j
     int b = (int)(r / k);
+    SP_BCHECK(idx[r], src_rows);  // a selected row (top-k index) inside its image's rows
     int64_t s = (int64_t)b * src_rows + idx[r];
     dst[r * ld_dst + c] = src[s * ld_src + c];
   }
@@ -365,6 +373,7 @@ __global__ void ref_init_kernel(const float* __restrict__ delta, int64_t ld, con
   for (int64_t i = gtid(); i < total; i += grid_stride()) {
     int c = (int)(i & 3);
     int64_t r = i >> 2;
+    SP_BCHECK(idx[r], 0x7fffffff);  // (the anchor count is not passed: at least not negative)
     float u = delta[r * ld + c] + anchors[(int64_t)idx[r] * 4 + c];
     ref[i] = sigmoidf_(u);
   }

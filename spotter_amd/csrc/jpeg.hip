@@ -121,6 +121,8 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const int16_t* __restric
   const int64_t local = blk - L.block_off[c];
   const int by = (int)(local / L.bw[c]), bx = (int)(local - (int64_t)by * L.bw[c]);
   const int64_t stride = (int64_t)L.bw[c] * 8;
+  SP_BCHECK(by, L.bh[c]);  // the block's position inside its component's block grid
+  SP_BCHECK(L.plane_off[c] + ((int64_t)by * 8 + t) * stride + (int64_t)bx * 8 + 7, L.plane_bytes);
   uint8_t* dst = work + L.plane_off[c] + ((int64_t)by * 8 + t) * stride + (int64_t)bx * 8;
   uint32_t w0 = 0, w1 = 0;
 #pragma unroll
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const sp_jpeg_layout L,
   if (i >= (int64_t)L.width * L.height) return;
   const int y = (int)(i / L.width), x = (int)(i - (int64_t)y * L.width);
   uint8_t* o = rgb + (int64_t)y * rgb_stride + (int64_t)x * 3;
+  SP_BCHECK(L.plane_off[0] + (int64_t)y * L.bw[0] * 8 + x, L.ncomp > 1 ? L.plane_off[1] : L.plane_bytes);
   const int yy = work[L.plane_off[0] + (int64_t)y * L.bw[0] * 8 + x];
   if (L.ncomp == 1) {
     o[0] = o[1] = o[2] = (uint8_t)yy;
@@ -182,6 +185,10 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(const sp_jpeg_layout L,
     const int rh = L.max_h / L.h[k], rv = L.max_v / L.v[k];
     const int dw = (int)(((int64_t)L.width * L.h[k] + L.max_h - 1) / L.max_h);
     const int dh = (int)(((int64_t)L.height * L.v[k] + L.max_v - 1) / L.max_v);
+    // the rows / columns chroma_at reads: [0, dh) × [0, dw) of a plane bw·8 wide and bh·8 high
+    SP_BCHECK((rv == 2 ? y >> 1 : y), (int64_t)L.bh[k] * 8);
+    SP_BCHECK((rh == 2 ? x >> 1 : x), dw);
+    SP_BCHECK(L.plane_off[k] + ((int64_t)L.bh[k] * 8 - 1) * L.bw[k] * 8 + L.bw[k] * 8 - 1, k == 1 && L.ncomp > 2 ? L.plane_off[2] : L.plane_bytes);
     cc[k - 1] = chroma_at(work + L.plane_off[k], (int64_t)L.bw[k] * 8, rh, rv, dw, dh, x, y);
   }
   if (L.color == 2) {  // RGB components: no conversion

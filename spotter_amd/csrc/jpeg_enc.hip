@@ -97,6 +97,8 @@ __global__ __launch_bounds__(256) void jpeg_fdct_kernel(const uint8_t* __restric
     int s[8];
     if (comp == 0) {  // luma: the edge-replicated plane (columns and rows past the image repeat the last one)
       const int y = min(by * 8 + r, H - 1);
+      SP_BCHECK(y, H);
+      SP_BCHECK(bx * 8, (int64_t)L.wb0 * 8);
       const uint8_t* row = rgb + (int64_t)y * stride;
 #pragma unroll
       for (int i = 0; i < 8; ++i) s[i] = rgb_y(row + (int64_t)min(bx * 8 + i, W - 1) * pb) - 128;
@@ -106,6 +108,8 @@ __global__ __launch_bounds__(256) void jpeg_fdct_kernel(const uint8_t* __restric
       // sample are clamped to the image (expand_right_edge, the row-group padding)
       const int cy = min(by * 8 + r, (H + L.v0 - 1) / L.v0 - 1);
       const int y0 = min(cy * L.v0, H - 1), y1 = min(cy * L.v0 + L.v0 - 1, H - 1);
+      SP_BCHECK(y0, H);
+      SP_BCHECK(y1, H);
       const uint8_t* r0 = rgb + (int64_t)y0 * stride;
       const uint8_t* r1 = rgb + (int64_t)y1 * stride;
 #pragma unroll
@@ -156,6 +160,7 @@ __global__ __launch_bounds__(256) void jpeg_fdct_kernel(const uint8_t* __restric
   __syncthreads();
   if (!live) return;
   // store: lane (j, r) writes zig-zag positions 8r .. 8r+7 of block j as one 16-byte piece
+  SP_BCHECK(mcu * L.bpm + j, (int64_t)L.mcux * L.mcuy * L.bpm);
   int16_t* dst = coefs + (mcu * L.bpm + j) * 64;
   int16_t v[8];
   if (!dummy) {
@@ -174,6 +179,7 @@ __global__ __launch_bounds__(256) void jpeg_fdct_kernel(const uint8_t* __restric
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = 0;
+    SP_BCHECK(src, L.bpm);
     if (r == 0) v[0] = (int16_t)qv[w][src][0];
   }
   int4 pk;
@@ -255,7 +261,7 @@ __global__ __launch_bounds__(256) void jpeg_mcu_bits_kernel(const int16_t* __res
 // total[0], then the words [0, ceil(total / 32)] of the bit buffer zeroed for the atomic ORs of the emit pass
 __global__ __launch_bounds__(1024) void jpeg_scan_kernel(const int32_t* __restrict__ bits, int64_t n,
                                                          int64_t* __restrict__ off, int64_t* __restrict__ total,
-                                                         uint32_t* __restrict__ words) {
+                                                         uint32_t* __restrict__ words, int64_t words_cap) {
   __shared__ int64_t part[1024];
   const int t = threadIdx.x;
   const int64_t chunk = (n + 1023) / 1024;
@@ -278,6 +284,7 @@ __global__ __launch_bounds__(1024) void jpeg_scan_kernel(const int32_t* __restri
   const int64_t tot = part[1023];
   if (t == 0) total[0] = tot;
   const int64_t nw = (tot + 31) / 32 + 1;
+  for (int64_t i = t; i < nw; i += 1024) SP_BCHECK(i, words_cap);
   for (int64_t i = t; i < nw; i += 1024) words[i] = 0;
 }
 
@@ -293,12 +300,14 @@ __global__ __launch_bounds__(256) void jpeg_emit_kernel(const int16_t* __restric
     acc |= (uint64_t)code << (64 - nacc - len);
     nacc += len;
     if (nacc >= 32) {
+      SP_BCHECK(wi, L.bits_cap / 4);  // the MCU's bits stay inside the layout's bit buffer bound
       atomicOr(words + wi, __builtin_bswap32((uint32_t)(acc >> 32)));
       acc <<= 32;
       nacc -= 32;
       ++wi;
     }
   });
+  if (nacc > 0) SP_BCHECK(wi, L.bits_cap / 4);
   if (nacc > 0) atomicOr(words + wi, __builtin_bswap32((uint32_t)(acc >> 32)));
 }
 
@@ -342,7 +351,7 @@ extern "C" int sp_jpeg_enc_rgb(const uint8_t* rgb, int64_t row_stride, int32_t p
   hipLaunchKernelGGL(jpeg_mcu_bits_kernel, dim3(g), dim3(256), 0, s, coefs, *lay, mbits);
   if ((rc = check_launch("sp_jpeg_enc_rgb(bits)"))) return rc;
   hipLaunchKernelGGL(jpeg_scan_kernel, dim3(1), dim3(1024), 0, s, mbits, nmcu, off, total,
-                     reinterpret_cast<uint32_t*>(bits));
+                     reinterpret_cast<uint32_t*>(bits), bits_cap / 4);
   if ((rc = check_launch("sp_jpeg_enc_rgb(scan)"))) return rc;
   hipLaunchKernelGGL(jpeg_emit_kernel, dim3(g), dim3(256), 0, s, coefs, *lay, off, reinterpret_cast<uint32_t*>(bits));
   if ((rc = check_launch("sp_jpeg_enc_rgb(emit)"))) return rc;

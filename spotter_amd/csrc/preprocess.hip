@@ -124,89 +124,135 @@ __device__ __forceinline__ int clip8(int acc) {
 // off and weigh 0, so the integer sums are unchanged). MAXT = 0: generic tap loop.
 // The u8 band buffer is dynamic LDS sized to the launch's tallest band (a 10-row band of a 640-wide
 // output needs 21 KB, not the 48 KB cap), so more workgroups share a CU and hide the byte-load latency.
+// Column tiles (round 6): a workgroup covers a band of T output rows × kColTile output columns (one column per
+// thread), so the LDS band holds rows × kColTile × 3 bytes instead of whole output rows and the grid has
+// bands × column tiles workgroups per image: a 4K source resized to 1280² is 400 workgroups of ~30 source rows
+// instead of 256 whole-width bands, each thread's chain of row loads 5× shorter.
+constexpr int kColTile = 256;
+
+// dword window of a thread's source bytes [p, p + 3·MAXT): NW aligned dwords from p & ~3 (clamped to the image's
+// last dword, whose bytes only feed taps of weight 0), re-aligned with v_alignbyte so byte b of the window is
+// bits 8(b & 3) of word b >> 2. Taps past the column's n weigh 0, so the integer sums are Pillow's.
+template <int MAXT>
+struct Window {
+  static constexpr int NW = (3 * MAXT + 6) / 4;
+  uint32_t w[NW];
+  __device__ __forceinline__ void load(const uint8_t* p, uintptr_t last) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uintptr_t base = a & ~uintptr_t(3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    uint32_t d[NW + 1];
+#pragma unroll
+    for (int k = 0; k <= NW; ++k) {
+      uintptr_t q = base + 4 * k;
+      q = q > last ? last : q;
+      d[k] = *reinterpret_cast<const uint32_t*>(q);
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  }
+  __device__ __forceinline__ int byte(int b) const { return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u); }
+};
+
+// Thread mapping: every pass walks output columns with the threads and rows with a loop, so the
+// per-column coefficients are loaded once and reused down the band (no index divisions).
+// MAXT > 0: every image of the launch has at most MAXT horizontal taps; the column's coefficients sit
+// in registers and its 3·MAXT source bytes of a row arrive as one dword window (taps past n weigh 0, so the
+// integer sums are unchanged). MAXT = 0: generic tap loop with byte loads.
+// The u8 band buffer is dynamic LDS sized to the launch's tallest band.
 template <int MAXT>
 __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
   extern __shared__ uint8_t tmp[];
   __shared__ float lut[256];
   const PreImg& im = a.img[blockIdx.y];
-  const int tile = blockIdx.x;
+  const int ow = a.out_w, oh = a.out_h;
+  const int ncol = (ow + kColTile - 1) / kColTile;
+  const int tile = blockIdx.x / ncol;
+  const int x0 = (blockIdx.x - tile * ncol) * kColTile;
   if (tile >= im.ntiles) return;
   // rescale table: f32(f64(v) * (1/255)), exactly IT:118-122's arithmetic
   lut[threadIdx.x] = (float)((double)threadIdx.x * (1.0 / 255.0));
-  const int ow = a.out_w, oh = a.out_h;
+  const int cw = min(kColTile, ow - x0);
   const int y0 = tile * im.rows_per_tile;
   const int y1 = min(y0 + im.rows_per_tile, oh);
   const int r0 = im.vb[2 * y0];
   const int r1 = im.vb[2 * (y1 - 1)] + im.vb[2 * (y1 - 1) + 1];
-  const int row_elems = ow * 3;
-  // horizontal pass: source rows [r0, r1) → tmp [row][x][c] (u8)
-  if constexpr (MAXT > 0) {
-    for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
-      const int xmin = im.hb[2 * xx];
-      const int n = im.hb[2 * xx + 1];
+  const int row_elems = cw * 3;
+  // the band's source rows lie inside the image (and the LDS band was sized for them on the host)
+  SP_BCHECK(r0, im.h);
+  SP_BCHECK(r1 - 1, im.h);
+  // horizontal pass: source rows [r0, r1) → tmp [row][x - x0][c] (u8)
+  const int xx = x0 + (int)threadIdx.x;
+  if (threadIdx.x < cw) {
+    const int xmin = im.hb[2 * xx];
+    const int n = im.hb[2 * xx + 1];
+    SP_BCHECK(xmin + n - 1, im.w);
+    uint8_t* t = tmp + threadIdx.x * 3;
+    if constexpr (MAXT > 0) {
+      SP_BCHECK(n, MAXT + 1);
       int kr[MAXT];
 #pragma unroll
       for (int j = 0; j < MAXT; ++j) kr[j] = j < n ? im.hk[xx * im.ksh + j] : 0;
       const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
-      uint8_t* t = tmp + xx * 3;
-#pragma unroll 8  // 8 source rows of byte loads in flight per thread: the pass is load-latency bound
+      const uintptr_t last = (reinterpret_cast<uintptr_t>(im.src + (int64_t)(im.h - 1) * im.stride + 3 * im.w - 1)) &
+                             ~uintptr_t(3);
+#pragma unroll 4  // four source rows of windows in flight per thread
       for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
+        Window<MAXT> win;
+        win.load(s, last);
         int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
 #pragma unroll
         for (int j = 0; j < MAXT; ++j) {
-          const bool ok = j < n;
-          a0 += (ok ? (int)s[3 * j] : 0) * kr[j];
-          a1 += (ok ? (int)s[3 * j + 1] : 0) * kr[j];
-          a2 += (ok ? (int)s[3 * j + 2] : 0) * kr[j];
+          a0 += win.byte(3 * j) * kr[j];
+          a1 += win.byte(3 * j + 1) * kr[j];
+          a2 += win.byte(3 * j + 2) * kr[j];
+        }
+        t[0] = (uint8_t)clip8(a0);
+        t[1] = (uint8_t)clip8(a1);
+        t[2] = (uint8_t)clip8(a2);
+      }
+    } else {
+      SP_BCHECK(n, im.ksh + 1);
+      const int* k = im.hk + xx * im.ksh;
+      const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
+#pragma unroll 4
+      for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
+        int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+        for (int j = 0; j < n; ++j) {
+          const int kj = k[j];
+          a0 += (int)s[3 * j] * kj;
+          a1 += (int)s[3 * j + 1] * kj;
+          a2 += (int)s[3 * j + 2] * kj;
         }
         t[0] = (uint8_t)clip8(a0);
         t[1] = (uint8_t)clip8(a1);
         t[2] = (uint8_t)clip8(a2);
       }
     }
-  } else
-  for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
-    const int xmin = im.hb[2 * xx];
-    const int n = im.hb[2 * xx + 1];
-    const int* k = im.hk + xx * im.ksh;
-    const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
-    uint8_t* t = tmp + xx * 3;
-#pragma unroll 4
-    for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
-      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
-      for (int j = 0; j < n; ++j) {
-        const int kj = k[j];
-        a0 += (int)s[3 * j] * kj;
-        a1 += (int)s[3 * j + 1] * kj;
-        a2 += (int)s[3 * j + 2] * kj;
-      }
-      t[0] = (uint8_t)clip8(a0);
-      t[1] = (uint8_t)clip8(a1);
-      t[2] = (uint8_t)clip8(a2);
-    }
   }
   __syncthreads();
   // vertical pass + rescale + CHW store (coalesced along x in each plane)
+  if (threadIdx.x >= cw) return;
   const int64_t plane = (int64_t)oh * ow;
-  for (int xx = threadIdx.x; xx < ow; xx += blockDim.x) {
-    float* o = im.out + (int64_t)y0 * ow + xx;
+  float* o = im.out + (int64_t)y0 * ow + xx;
 #pragma unroll 4
-    for (int yy = y0; yy < y1; ++yy, o += ow) {
-      const int ymin = im.vb[2 * yy] - r0;
-      const int n = im.vb[2 * yy + 1];
-      const int* k = im.vk + yy * im.ksv;
-      const uint8_t* t = tmp + ymin * row_elems + xx * 3;
-      int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
-      for (int j = 0; j < n; ++j, t += row_elems) {
-        const int kj = k[j];
-        a0 += (int)t[0] * kj;
-        a1 += (int)t[1] * kj;
-        a2 += (int)t[2] * kj;
-      }
-      o[0] = lut[clip8(a0)];
-      o[plane] = lut[clip8(a1)];
-      o[2 * plane] = lut[clip8(a2)];
+  for (int yy = y0; yy < y1; ++yy, o += ow) {
+    const int ymin = im.vb[2 * yy] - r0;
+    const int n = im.vb[2 * yy + 1];
+    SP_BCHECK(ymin, r1 - r0);  // the vertical taps read rows of this band's LDS buffer
+    SP_BCHECK(ymin + n - 1, r1 - r0);
+    const int* k = im.vk + yy * im.ksv;
+    const uint8_t* t = tmp + ymin * row_elems + threadIdx.x * 3;
+    int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+    for (int j = 0; j < n; ++j, t += row_elems) {
+      const int kj = k[j];
+      a0 += (int)t[0] * kj;
+      a1 += (int)t[1] * kj;
+      a2 += (int)t[2] * kj;
     }
+    o[0] = lut[clip8(a0)];
+    o[plane] = lut[clip8(a1)];
+    o[2 * plane] = lut[clip8(a2)];
   }
 }
 
@@ -225,6 +271,8 @@ __global__ __launch_bounds__(256) void preprocess_same_size_kernel(const PreArgs
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (int64_t)oh * q4; i += (int64_t)gridDim.x * 256) {
     const int y = (int)(i / q4);
     const int x = (int)(i - (int64_t)y * q4) * 4;
+    SP_BCHECK(y, oh);
+    SP_BCHECK(x + 3, ow);
     const uint32_t* s = reinterpret_cast<const uint32_t*>(im.src + (int64_t)y * im.stride + x * 3);
     const uint32_t w0 = s[0], w1 = s[1], w2 = s[2];  // r0 g0 b0 r1 | g1 b1 r2 g2 | b2 r3 g3 b3
     float* o = im.out + (int64_t)y * ow + x;
@@ -276,7 +324,7 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
                                 void* stream) {
   using namespace sp;
   SP_ARG_CHECK(images && out && n > 0, "sp_preprocess_u8: null args");
-  SP_ARG_CHECK(out_h > 0 && out_w > 0 && out_w * 3 <= kLdsBytes, "sp_preprocess_u8: bad out size");
+  SP_ARG_CHECK(out_h > 0 && out_w > 0, "sp_preprocess_u8: bad out size");
   hipStream_t s = as_stream(stream);
   for (int base = 0; base < n; base += kMaxImgs) {
     PreArgs a;
@@ -316,11 +364,15 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
         return -3;
       }
       int ntiles = 0;
-      int T = band_rows(*vc, out_h, out_w * 3, &ntiles);
+      const int cwmax = std::min(out_w, kColTile);
+      int T = band_rows(*vc, out_h, cwmax * 3, &ntiles);
       SP_ARG_CHECK(T > 0, "sp_preprocess_u8: %dx%d -> %dx%d needs more LDS than available",
                    im.height, im.width, out_h, out_w);
-      // shorter bands when the batch is small, so the launch still spreads over ~2k workgroups
-      const int cap = std::max(4, (out_h * cnt + 2047) / 2048);
+      // shorter bands when the batch is small, so the launch still spreads over ~2k workgroups (bands × column
+      // tiles × images), but at least 8 output rows per band where the LDS allows (the band's extra source rows,
+      // ~2 at any scale, are read twice)
+      const int ncol = (out_w + kColTile - 1) / kColTile;
+      const int cap = std::max(8, (out_h * cnt * ncol + 2047) / 2048);
       if (T > cap) {
         T = cap;
         ntiles = (out_h + T - 1) / T;
@@ -328,7 +380,7 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       for (int y0 = 0; y0 < out_h; y0 += T) {  // LDS bytes of this image's tallest band
         const int y1 = y0 + T < out_h ? y0 + T : out_h;
         const int rows = vc->h_bounds[2 * (y1 - 1)] + vc->h_bounds[2 * (y1 - 1) + 1] - vc->h_bounds[2 * y0];
-        if (rows * out_w * 3 > lds) lds = rows * out_w * 3;
+        if (rows * cwmax * 3 > lds) lds = rows * cwmax * 3;
       }
       PreImg& p = a.img[i];
       p.src = im.data;
@@ -347,7 +399,7 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       if (ntiles > max_tiles) max_tiles = ntiles;
       if (hc->ksize > max_ksh) max_ksh = hc->ksize;
     }
-    const dim3 grid(max_tiles, cnt);
+    const dim3 grid(max_tiles * ((out_w + kColTile - 1) / kColTile), cnt);
     lds = (lds + 15) & ~15;
     if (max_ksh <= 3)  // up-scaling and same-size sources
       hipLaunchKernelGGL(preprocess_kernel<3>, grid, dim3(256), lds, s, a);

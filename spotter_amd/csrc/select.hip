@@ -156,6 +156,7 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     const uint32_t key = keys[i];
     if (key > T) {
       const uint32_t pos = atomicAdd(&s_sel[2], 1u);
+      SP_BCHECK(pos, k);  // exactly n_gt = k - need_eq keys lie above the threshold key
       cand[pos] = ((unsigned long long)key << 32) | (0xffffffffu - (uint32_t)i);
     } else if (key == T) {
       atomicAdd(&s_sel[3], 1u);
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     for (int i = tid; i < n; i += kThreads)
       if (keys[i] == T) {
         const uint32_t pos = atomicAdd(&s_sel[2], 1u);
+        SP_BCHECK(pos, k);
         cand[pos] = ((unsigned long long)T << 32) | (0xffffffffu - (uint32_t)i);
       }
   } else {
@@ -202,6 +204,8 @@ __global__ __launch_bounds__(kThreads) void topk_kernel(const float* __restrict_
     for (int j = 0; j < k; ++j) rank += cand[j] > e;
     const uint32_t key = (uint32_t)(e >> 32);
     const uint32_t id = 0xffffffffu - (uint32_t)(e & 0xffffffffu);
+    SP_BCHECK(rank, k);
+    SP_BCHECK(id, n);  // an unfilled candidate slot (0) would decode to index 2^32 - 1
     idx_out[row * k + rank] = (int32_t)id;
     if (vals) vals[row * k + rank] = key2f(key);
   }
@@ -219,6 +223,7 @@ __global__ __launch_bounds__(512) void decode_kernel(const float* __restrict__ b
   const float ih = (float)target_hw[2 * b], iw = (float)target_hw[2 * b + 1];
   for (int i = threadIdx.x; i < k; i += blockDim.x) {
     const int32_t id = idx[(int64_t)b * k + i];
+    SP_BCHECK(id, (int64_t)q * c);
     const int lab = id % c;
     const int qq = id / c;
     const float* bx = boxes + ((int64_t)b * q + qq) * 4;

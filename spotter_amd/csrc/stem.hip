@@ -45,6 +45,7 @@ __global__ __launch_bounds__(STEM_BLOCK) void stem_conv_nchw_kernel(
     const int oy = (int)(q % ho);
     const int b = (int)(q / ho);
     const int64_t hw = (int64_t)h * w;
+    SP_BCHECK(b, n);
     const float* xb = x + (int64_t)b * 3 * hw;
 
     float in[27];
@@ -196,6 +197,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c32_bf16_kernel(const uint16_t
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
+    SP_BCHECK(b, nimg);
     const int oy0 = ty * TH, ox0 = tx * C3_TW;
 #pragma unroll
     for (int k = 0; k < PFN; ++k) {
@@ -215,6 +218,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_c32_bf16_kernel(const uint16_t
   t /= tiles_x;
   const int ty = (int)(t % tiles_y);
   const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
   const int oy0 = ty * TH, ox0 = tx * C3_TW;
   __syncthreads();  // the previous tile's halo reads are done
 #pragma unroll
@@ -381,6 +385,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c32_f32_kernel(const float* __
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
+    SP_BCHECK(b, nimg);
     const int oy0 = ty * F3_TH, ox0 = tx * C3_TW;
 #pragma unroll
     for (int k = 0; k < F3_PF; ++k) {
@@ -416,6 +422,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c32_f32_kernel(const float* __
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
+    SP_BCHECK(b, nimg);
     const int oy = ty * F3_TH + wave, ox0 = tx * C3_TW;
     f32x16_s acc[TMN][2];
 #pragma unroll
@@ -557,6 +565,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
+    SP_BCHECK(b, nimg);
     const int oy0 = ty * B6_TH, ox0 = tx * B6_TW;
 #pragma unroll
     for (int k = 0; k < B6_PF; ++k) {
@@ -591,6 +601,8 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     t /= tiles_x;
     const int ty = (int)(t % tiles_y);
     const int b = (int)(t / tiles_y);
+  SP_BCHECK(b, nimg);
+    SP_BCHECK(b, nimg);
     const int oy0 = ty * B6_TH + 2 * wave, ox = tx * B6_TW + r;
     int64_t pix[2];
     bool in[2];
@@ -598,6 +610,7 @@ __global__ __launch_bounds__(512, 1) void conv3x3_c64_bf16_kernel(const uint16_t
     for (int j = 0; j < 2; ++j) {
       in[j] = oy0 + j < h && ox < w;
       pix[j] = in[j] ? ((int64_t)b * h + oy0 + j) * w + ox : 0;
+      if (in[j]) SP_BCHECK(pix[j], (int64_t)nimg * h * w);
     }
     uint4 rq[2][2][2];  // [row j][channel half i][16-channel group p]: this lane's 8 residual channels
     auto fetch_res = [&]() {

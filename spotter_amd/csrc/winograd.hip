@@ -53,6 +53,7 @@ __global__ __launch_bounds__(256) void wino_in_f23_x2_kernel(const float* __rest
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int yy = y0 + i, xx = x0 + j;
+        if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w) SP_BCHECK((b * h + yy) * w + xx, nb * h * w);
         d[i][j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
                       ? *reinterpret_cast<const float4*>(x + ((b * h + yy) * w + xx) * lda + c)
                       : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -68,6 +69,8 @@ __global__ __launch_bounds__(256) void wino_in_f23_x2_kernel(const float* __rest
         q[i][2] = d[i][2 * k + 2] - d[i][2 * k + 1];
         q[i][3] = d[i][2 * k + 1] - d[i][2 * k + 3];
       }
+      SP_BCHECK((b * th + ty) * tw + tx0 + k, T);
+      SP_BCHECK(c + 3, cin);
       float* dst = V + ((b * th + ty) * tw + tx0 + k) * cin + c;
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb) {
@@ -110,6 +113,7 @@ __global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restri
     const int r = (int)(t - b * th * tw);
     const int ty = r / tw;
     const int tx = r - ty * tw;
+    SP_BCHECK(n + 3, cout);
     const float* src = Mc + t * cout + n;
     float4 mm[4][4];
 #pragma unroll
@@ -130,6 +134,7 @@ __global__ __launch_bounds__(256) void wino_out_f23_kernel(const float* __restri
       const float4 y0 = s[p][0] + s[p][1] + s[p][2];
       const float4 y1 = s[p][1] - s[p][2] - s[p][3];
       const int64_t m0 = (b * d.Ho + oy) * d.Wo + 2 * tx;
+      SP_BCHECK(m0, (int64_t)d.N * d.Ho * d.Wo);
       *reinterpret_cast<float4*>(d.C + m0 * d.ldc + n) = epi4(y0, d, m0, n);
       if (2 * tx + 1 < d.Wo) *reinterpret_cast<float4*>(d.C + (m0 + 1) * d.ldc + n) = epi4(y1, d, m0 + 1, n);
     }
@@ -184,6 +189,7 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
 #pragma unroll
       for (int j = 0; j < 6; ++j) {
         const int xx = x0 + j;
+        if ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w) SP_BCHECK((b * h + yy) * w + xx, (T / ((int64_t)th * tw)) * h * w);
         dr[j] = ((unsigned)yy < (unsigned)h && (unsigned)xx < (unsigned)w)
                     ? *reinterpret_cast<const vf*>(x + ((b * h + yy) * w + xx) * lda + c)
                     : vf(0.f);
@@ -198,6 +204,9 @@ __global__ __launch_bounds__(256) void wino_in_f43_kernel(const float* __restric
       }
     }
     float* dst = V + t * tstride + c;
+    // the last component's element of this (tile, channel group) inside the 36·T·Cin V region
+    SP_BCHECK(35 * plane + t * tstride + c + VW - 1, 36 * plane);
+    SP_BCHECK(c + VW - 1, tstride);
 #pragma unroll
     for (int bb = 0; bb < 6; ++bb)
 #pragma unroll
@@ -226,6 +235,8 @@ __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restri
     const int ty = r / tw;
     const int tx = r - ty * tw;
     const float* src = Mc + t * tstride + n;
+    SP_BCHECK(35 * plane + t * tstride + n + VW - 1, 36 * plane);
+    SP_BCHECK(n + VW - 1, d.Cout);
     vf s[4][6];  // s[p][bb] = Σ_a Aᵀ[p][a] M[a][bb], accumulated as the rows of M arrive
 #pragma unroll
     for (int p = 0; p < 4; ++p)
@@ -258,6 +269,7 @@ __global__ __launch_bounds__(256) void wino_out_f43_kernel(const float* __restri
         for (int bb = 0; bb < 6; ++bb)
           if (kAT43[qq][bb] != 0.f) y = __builtin_elementwise_fma(vf(kAT43[qq][bb]), s[p][bb], y);
         const int64_t m = (b * d.Ho + oy) * d.Wo + ox;
+        SP_BCHECK(m, (int64_t)d.N * d.Ho * d.Wo);
         y = __builtin_elementwise_fma(y, sc, sh);
         if (d.res1) y += *reinterpret_cast<const vf*>(d.res1 + m * d.ldr1 + n);
 #pragma unroll

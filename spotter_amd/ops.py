@@ -484,7 +484,8 @@ def msda(value: V, value_col: int, off_aw: V, ref: torch.Tensor, out: V, B, S, Q
     nbytes = value.t.element_size() * B * value_bytes + 4 * B * Q * (heads * L * points * 3 + 4 + heads * head_dim)
     # per sample: 4 bilinear taps (multiply-add) + the attention weight
     flops = B * Q * heads * L * points * head_dim * 10
-    _launch("msda", "sp_msda", (C.byref(d), stream()), flops, nbytes, (B, S, Q, heads, head_dim, L, points))
+    _launch("msda", "sp_msda", (C.byref(d), stream()), flops, nbytes,
+            (B, S, Q, heads, head_dim, L, points, value.t.element_size()))
 
 
 def topk_rows(x: V, rows, n, k, idx: torch.Tensor, vals: torch.Tensor | None = None, reduce_c=1,

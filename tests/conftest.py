@@ -31,7 +31,46 @@ def pytest_collection_modifyitems(config, items):
             it.add_marker(skip)
 
 
+_BOUNDS_LOG = []
+
+
+@pytest.fixture(autouse=True)
+def _bounds_check(request):
+    """Bounds-check library (SPOTTER_HIP_LIB=spotter_amd/_bounds/libspotter_bounds.so, SP_BUILD_BOUNDS): after
+    every GPU test, collect the kernels' index violations (sp_bounds_report); any hit fails that test. With the
+    product library this does nothing."""
+    yield
+    if "gpu" not in request.node.keywords or not os.environ.get("SPOTTER_HIP_LIB"):
+        return
+    import ctypes
+
+    from spotter_amd._lib import SP_BUILD_BOUNDS, lib
+
+    L = lib()
+    if not L.sp_build_flags() & SP_BUILD_BOUNDS:
+        return
+    buf = ctypes.create_string_buffer(8192)
+    hits = L.sp_bounds_report(buf, len(buf))
+    _BOUNDS_LOG.append({"test": request.node.nodeid, "hits": int(hits),
+                        "report": buf.value.decode(errors="replace")})
+    assert hits == 0, f"bounds-check build: {hits} index violations\n{buf.value.decode(errors='replace')}"
+
+
 def pytest_sessionfinish(session, exitstatus):
+    if _BOUNDS_LOG:
+        import json
+
+        out = os.path.join(ROOT, "gpurun_out", "bounds_report.json")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        with open(out, "w") as f:
+            json.dump({"tests": len(_BOUNDS_LOG), "tests_with_hits": sum(1 for r in _BOUNDS_LOG if r["hits"]),
+                       "total_hits": sum(max(0, r["hits"]) for r in _BOUNDS_LOG),
+                       "hits": [r for r in _BOUNDS_LOG if r["hits"]]}, f, indent=1)
+        print(f"\nbounds report -> {out}")
+    _write_margins()
+
+
+def _write_margins():
     """Write the observed parity margins of the golden tests (tests/margins.py), if any ran."""
     here = os.path.dirname(os.path.abspath(__file__))
     if here not in sys.path:

@@ -984,6 +984,39 @@ def test_msda_bf16_value_rows(dev):
     assert d <= 1e-6 * np.abs(outs[0]).max(), d
 
 
+@pytest.mark.parametrize("bf16", [False, True])
+def test_msda_point_sharing_kernel_is_bit_identical(dev, bf16):
+    """msda_h8_kernel (the decoder's shape: 8 heads × 32, 3 levels × 4 points; each point's location math done
+    once by its owner lane and shared) against msda_vec_kernel (every lane repeats it), selected with
+    sp_set_tuning(SP_TUNE_MSDA_GENERIC): bit-identical outputs, including points far outside the map, for fp32
+    and bf16 value rows in the engine's value_all layout (6 layers side by side)."""
+    from spotter_amd import ops
+    from spotter_amd._lib import lib
+    from spotter_amd.ops import V
+
+    rng = np.random.default_rng(21)
+    B, Q, nH, dh, nL, nP = 3, 300, 8, 32, 3, 4
+    shapes, starts, S = [(20, 20), (10, 10), (5, 5)], [0, 400, 500], 525
+    D = nH * dh
+    vals = rng.standard_normal((B * S, 6 * D)).astype(np.float32)
+    offaw = np.concatenate([rng.standard_normal((B * Q, nH * nL * nP * 2)) * 3.0,
+                            rng.standard_normal((B * Q, nH * nL * nP)) * 2.0], 1).astype(np.float32)
+    ref = np.concatenate([rng.uniform(0.0, 1.0, (B * Q, 2)), rng.uniform(0.01, 0.9, (B * Q, 2))], 1).astype(np.float32)
+    value = V(T((_bf16_rows(vals)[0] if bf16 else vals).reshape(-1), dev), 0, 6 * D)  # int16 rows = bf16
+    outs = []
+    try:
+        for generic in (1, 0):
+            assert lib().sp_set_tuning(4, generic) == 0
+            out = torch.full((B * Q * D,), float("nan"), device=dev)
+            ops.msda(value, 3 * D, V(T(offaw.reshape(-1), dev), 0, offaw.shape[1]), T(ref, dev), V(out, 0, D),
+                     B, S, Q, nH, dh, shapes, starts, nP, 0.5)
+            outs.append(out.cpu().numpy())
+    finally:
+        lib().sp_set_tuning(4, 0)
+    assert np.isfinite(outs[1]).all()
+    assert np.array_equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("pad", [0, 1])
 def test_msda_matches_oracle(dev, pad):
     """MSDA core incl. out-of-range sampling points (zero padding) vs oracle.grid_sample_bilinear.
@@ -1087,6 +1120,36 @@ def test_preprocess_bit_exact(dev, out):
     got = res.cpu().numpy().reshape(len(imgs), 3, out, out)
     for i, im in enumerate(imgs):
         np.testing.assert_array_equal(got[i], preprocess(im, (out, out)), err_msg=str(PRE_SIZES[i]))
+
+
+@pytest.mark.parametrize("oh,ow", [(640, 640), (300, 517), (77, 1000), (1280, 700), (5, 3)])
+def test_preprocess_unaligned_sources_and_ragged_column_tiles(dev, oh, ow):
+    """Sources carved out of one uint8 buffer at odd byte offsets (so no row starts 4-byte aligned and the last
+    image ends at the buffer's end: the dword windows' clamp), odd widths, output widths that are not a multiple
+    of the 256-column tile, a single-image launch; bit-exact with the Pillow oracle."""
+    from oracle.pil_resize import preprocess
+    from spotter_amd import ops
+    from spotter_amd.synthetic import synthetic_image
+
+    sizes = [(717, 1200), (33, 2999), (640, 641), (1, 7), (1080, 1920)]
+    imgs = [synthetic_image(13 * h + w, h, w) for h, w in sizes]
+    offs, pos = [], 3
+    for im in imgs:
+        offs.append(pos)
+        pos += im.size + 1
+    pos -= 1  # the last image ends exactly at the end of the buffer
+    buf = np.zeros(pos, np.uint8)
+    for o, im in zip(offs, imgs):
+        buf[o:o + im.size] = im.reshape(-1)
+    dbuf = T(buf, dev)
+    views = [dbuf[o:o + im.size].view(im.shape) for o, im in zip(offs, imgs)]
+    want = [preprocess(im, (oh, ow)) for im in imgs]
+    for batch, exp in ((views, want), (views[-1:], want[-1:])):
+        res = torch.empty(len(batch) * 3 * oh * ow, device=dev)
+        ops.preprocess_u8(batch, res, oh, ow)
+        got = res.cpu().numpy().reshape(len(batch), 3, oh, ow)
+        for i, e in enumerate(exp):
+            np.testing.assert_array_equal(got[i], e, err_msg=str(batch[i].shape))
 
 
 @pytest.mark.parametrize("out", [640, 1280, 36])

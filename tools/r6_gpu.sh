@@ -18,3 +18,21 @@ if [ "$PART" = serve ]; then
   tail -5 $OUT/pmc_x3.log
   echo r6 serve done
 fi
+if [ "$PART" = bounds ]; then
+  # product library: GPU suite + MSDA A/B; then the bounds-check library over the same suite; then the served sweep
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests.log 2>&1
+  tail -1 $OUT/gpu_tests.log
+  timeout -k 10 300 python3 -u tools/microbench/msda_ab.py --out $OUT/msda_ab.json > $OUT/msda_ab.log 2>&1
+  cat $OUT/msda_ab.log | grep -v amdgpu.ids | cut -c1-300
+  set +e
+  SPOTTER_HIP_LIB=spotter_amd/_bounds/libspotter_bounds.so timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/gpu_tests_bounds.log 2>&1
+  rc=$?
+  set -e
+  tail -3 $OUT/gpu_tests_bounds.log
+  # test failures (rc 1) are the report; a crash, abort or time limit ends the call here
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "bounds suite rc=$rc: stopping"; exit $rc; fi
+  cp gpurun_out/bounds_report.json $OUT/bounds_report.json 2>/dev/null || true
+  timeout -k 10 900 python3 -u tools/served_sweep.py --k 6 8 12 --precision bf16 fp32 --seconds 8 --out $OUT/served > $OUT/served.log 2>&1
+  grep -v amdgpu.ids $OUT/served.log | cut -c1-240
+  echo r6 bounds done
+fi
