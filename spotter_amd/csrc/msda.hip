@@ -168,8 +168,10 @@ __global__ __launch_bounds__(256) void msda_vec_kernel(const sp_msda_desc d, con
 // all 12 twice per lane), the softmax sum in the vec kernel's sequential order from the 12 values shuffled in,
 // and the location / bilinear weights / clamped corner rows of points j and j + 8; every lane then takes each
 // point's 4 corner rows, 4 weights and attention weight from its owner lane (ds_bpermute) and gathers and
-// accumulates exactly as before. Same operations in the same order on the same values: bit-identical outputs
-// (tests/test_gpu_kernels.py::test_msda_*), 1/8 of the location math and 1/12 of the exponentials per lane.
+// accumulates exactly as before. Same operations in the same order on the same values: bit-identical outputs on
+// fp32 value rows (tests/test_gpu_kernels.py::test_msda_point_sharing_kernel_is_bit_identical; on bf16 rows the
+// compiler contracts the corner sums into fmas differently in the two instantiations: within fp32 rounding),
+// 1/8 of the location math and 1/12 of the exponentials per lane.
 template <typename VT>
 __global__ __launch_bounds__(256) void msda_h8_kernel(const sp_msda_desc d, const VT* __restrict__ value) {
   constexpr int LPH = 8, LP = 12, P = 4;

@@ -988,8 +988,9 @@ def test_msda_bf16_value_rows(dev):
 def test_msda_point_sharing_kernel_is_bit_identical(dev, bf16):
     """msda_h8_kernel (the decoder's shape: 8 heads × 32, 3 levels × 4 points; each point's location math done
     once by its owner lane and shared) against msda_vec_kernel (every lane repeats it), selected with
-    sp_set_tuning(SP_TUNE_MSDA_GENERIC): bit-identical outputs, including points far outside the map, for fp32
-    and bf16 value rows in the engine's value_all layout (6 layers side by side)."""
+    sp_set_tuning(SP_TUNE_MSDA_GENERIC), including points far outside the map, in the engine's value_all layout
+    (6 layers side by side): bit-identical for fp32 value rows; for bf16 rows the two instantiations contract the
+    corner sums into fmas differently (as test_msda_bf16_value_rows notes), so there the bar is fp32 rounding."""
     from spotter_amd import ops
     from spotter_amd._lib import lib
     from spotter_amd.ops import V
@@ -1014,7 +1015,10 @@ def test_msda_point_sharing_kernel_is_bit_identical(dev, bf16):
     finally:
         lib().sp_set_tuning(4, 0)
     assert np.isfinite(outs[1]).all()
-    assert np.array_equal(outs[0], outs[1])
+    if bf16:
+        assert np.abs(outs[0] - outs[1]).max() <= 1e-6 * np.abs(outs[0]).max()
+    else:
+        assert np.array_equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("pad", [0, 1])
@@ -1223,3 +1227,32 @@ def test_linear_fused_layernorm(dev, rows, k, n):
     ops.linear(view(T(x.reshape(-1), dev), k), rows, k, T(w, dev), n, view(out, n), bias=T(b, dev),
                res1=view(T(res.reshape(-1), dev), n), row_scale=T(rs, dev), ln=(T(g, dev), T(be, dev), 1e-5))
     np.testing.assert_allclose(out.cpu().numpy().reshape(rows, n), ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.skipif("_bounds" not in os.environ.get("SPOTTER_HIP_LIB", ""),
+                    reason="bounds-check library only (SPOTTER_HIP_LIB=spotter_amd/_bounds/libspotter_bounds.so)")
+def test_bounds_build_reports_a_violation(dev):
+    """Positive control of the bounds-check build: a top-k index one past its image's rows makes
+    sp_gather_rows read the next image's first row — inside the buffer, so no memory fault — and the
+    SP_BCHECK there must count it, with its source unit, line, index and extent; the report then resets."""
+    import ctypes
+
+    from spotter_amd import ops
+    from spotter_amd._lib import SP_BUILD_BOUNDS, lib
+    from spotter_amd.ops import V
+
+    L = lib()
+    assert L.sp_build_flags() & SP_BUILD_BOUNDS
+    buf = ctypes.create_string_buffer(4096)
+    assert L.sp_bounds_report(buf, len(buf)) == 0  # clean before
+    src_rows, d, k = 10, 8, 3
+    src = torch.arange(2 * src_rows * d, dtype=torch.float32, device=dev)
+    idx = torch.tensor([0, 9, src_rows, 1, 2, 3], dtype=torch.int32, device=dev)  # image 0's third index: one past
+    dst = torch.empty(2 * k * d, device=dev)
+    ops.gather_rows(V(src, 0, d), src_rows, idx, k, 2, d, V(dst, 0, d))
+    hits = L.sp_bounds_report(buf, len(buf))
+    rep = buf.value.decode()
+    assert hits == d, rep  # one check per gathered element of the bad row
+    assert "elementwise.hip" in rep and f"index={src_rows} extent={src_rows}" in rep, rep
+    assert L.sp_bounds_report(buf, len(buf)) == 0  # reset
+    np.testing.assert_array_equal(dst.view(2 * k, d)[2].cpu().numpy(), src.view(-1, d)[src_rows].cpu().numpy())

@@ -469,7 +469,9 @@ def test_rayservice_template_renders():
     app = serve["applications"][0]
     assert (app["name"], app["import_path"], app["route_prefix"]) == ("spotter-serve", "spotter.serve:deployment", "/detect")
     dep = app["deployments"][0]
-    assert dep["name"] == "AmenitiesDetector" and dep["ray_actor_options"]["num_gpus"] == 1
+    assert dep["name"] == "AmenitiesDetector"
+    per_gpu = round(1 / dep["ray_actor_options"]["num_gpus"])
+    assert per_gpu * dep["ray_actor_options"]["num_gpus"] == 1
     rc = doc["spec"]["rayClusterConfig"]
     head = rc["headGroupSpec"]["template"]["spec"]["containers"][0]
     assert head["image"] == image and rc["headGroupSpec"]["rayStartParams"]["num-gpus"] == "0"
@@ -478,7 +480,17 @@ def test_rayservice_template_renders():
     assert worker["image"] == image
     gpus = worker["resources"]["limits"]["amd.com/gpu"]
     assert worker["resources"]["requests"]["amd.com/gpu"] == gpus
-    assert int(wg["rayStartParams"]["num-gpus"]) == gpus == dep["num_replicas"] == 8
+    assert int(wg["rayStartParams"]["num-gpus"]) == gpus == 8 and dep["num_replicas"] == gpus * per_gpu
+    # replicas per GPU = the measured k-sweep's (profiles/r6/served, C4's bf16 and the fp32 parity path): the most
+    # whole-request throughput whose p95 stays within 1.5x the single replica's
+    import json
+
+    for prec in ("bf16", "fp32"):
+        with open(os.path.join(ROOT, "profiles", "r6", "served", f"served_r101vd_{prec}.json")) as f:
+            pts = json.load(f)["points"]
+        one = next(p for p in pts if p["k_processes"] == 1)
+        ok = [p for p in pts if p["p95_ms"] <= 1.5 * one["p95_ms"]]
+        assert max(ok, key=lambda p: p["img_per_s"])["k_processes"] == per_gpu, prec
     env = {e["name"]: e["value"] for e in worker["env"]}
     assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     # as the reference template (configs/rayservice-template.yaml:41-59): no pod overrides MODEL_NAME,

@@ -76,7 +76,8 @@ def main():
         res[name] = {"B": B, "size": size, "bf16": bf16, "ms_h8": round(ms_new, 4), "ms_vec": round(ms_old, 4),
                      "speedup": round(ms_old / ms_new, 3), "gather_gbps_h8": round(gathered / ms_new / 1e6, 1),
                      "gather_gbps_vec": round(gathered / ms_old / 1e6, 1),
-                     "bit_identical": bool(torch.equal(outs[0], outs[1]))}
+                     "bit_identical": bool(torch.equal(outs[0], outs[1])),
+                     "max_rel_diff": float((outs[0] - outs[1]).abs().max() / outs[1].abs().max())}
         print(json.dumps({name: res[name]}), flush=True)
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
