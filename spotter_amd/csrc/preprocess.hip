@@ -110,6 +110,7 @@ struct PreImg {
 struct PreArgs {
   PreImg img[kMaxImgs];
   int out_h, out_w;
+  int vec4;  // out_w % 4 == 0 and a 16-byte aligned output: the vertical pass stores float4s
 };
 
 __device__ __forceinline__ int clip8(int acc) {
@@ -196,10 +197,9 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
       const uint8_t* s = im.src + (int64_t)r0 * im.stride + xmin * 3;
       const uintptr_t last = (reinterpret_cast<uintptr_t>(im.src + (int64_t)(im.h - 1) * im.stride + 3 * im.w - 1)) &
                              ~uintptr_t(3);
-#pragma unroll 4  // four source rows of windows in flight per thread
-      for (int rr = r0; rr < r1; ++rr, s += im.stride, t += row_elems) {
-        Window<MAXT> win;
-        win.load(s, last);
+      // groups of RG rows: every row's window loads are issued before any of them is used
+      constexpr int RG = 4;
+      auto row_out = [&](const Window<MAXT>& win, uint8_t* tt) {
         int a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
 #pragma unroll
         for (int j = 0; j < MAXT; ++j) {
@@ -207,9 +207,22 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
           a1 += win.byte(3 * j + 1) * kr[j];
           a2 += win.byte(3 * j + 2) * kr[j];
         }
-        t[0] = (uint8_t)clip8(a0);
-        t[1] = (uint8_t)clip8(a1);
-        t[2] = (uint8_t)clip8(a2);
+        tt[0] = (uint8_t)clip8(a0);
+        tt[1] = (uint8_t)clip8(a1);
+        tt[2] = (uint8_t)clip8(a2);
+      };
+      int rr = r0;
+      for (; rr + RG <= r1; rr += RG, s += RG * (int64_t)im.stride, t += RG * row_elems) {
+        Window<MAXT> win[RG];
+#pragma unroll
+        for (int g = 0; g < RG; ++g) win[g].load(s + g * (int64_t)im.stride, last);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) row_out(win[g], t + g * row_elems);
+      }
+      for (; rr < r1; ++rr, s += im.stride, t += row_elems) {
+        Window<MAXT> win;
+        win.load(s, last);
+        row_out(win, t);
       }
     } else {
       SP_BCHECK(n, im.ksh + 1);
@@ -232,8 +245,39 @@ __global__ __launch_bounds__(256) void preprocess_kernel(const PreArgs a) {
   }
   __syncthreads();
   // vertical pass + rescale + CHW store (coalesced along x in each plane)
-  if (threadIdx.x >= cw) return;
   const int64_t plane = (int64_t)oh * ow;
+  if (a.vec4) {
+    // four adjacent columns per thread (12 band bytes = 3 aligned LDS dwords per tap), float4 stores per plane;
+    // the four 64-thread groups take every fourth output row. Same integer sums: bit-identical.
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int xl = 4 * tx;
+    if (xl >= cw) return;
+    float* ob = im.out + x0 + xl;
+    for (int yy = y0 + ty; yy < y1; yy += 4) {
+      const int ymin = im.vb[2 * yy] - r0;
+      const int n = im.vb[2 * yy + 1];
+      SP_BCHECK(ymin, r1 - r0);
+      SP_BCHECK(ymin + n - 1, r1 - r0);
+      const int* k = im.vk + yy * im.ksv;
+      const uint32_t* tp = reinterpret_cast<const uint32_t*>(tmp + ymin * row_elems + xl * 3);
+      int acc[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) acc[i] = 1 << (kPrecisionBits - 1);
+      for (int j = 0; j < n; ++j, tp += row_elems / 4) {
+        const int kj = k[j];
+        const uint32_t u[3] = {tp[0], tp[1], tp[2]};
+#pragma unroll
+        for (int i = 0; i < 12; ++i) acc[i] += (int)((u[i >> 2] >> (8 * (i & 3))) & 255u) * kj;
+      }
+      float* o = ob + (int64_t)yy * ow;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        *reinterpret_cast<float4*>(o + c * plane) = make_float4(lut[clip8(acc[c])], lut[clip8(acc[3 + c])],
+                                                                lut[clip8(acc[6 + c])], lut[clip8(acc[9 + c])]);
+    }
+    return;
+  }
+  if (threadIdx.x >= cw) return;
   float* o = im.out + (int64_t)y0 * ow + xx;
 #pragma unroll 4
   for (int yy = y0; yy < y1; ++yy, o += ow) {
@@ -372,7 +416,11 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       // tiles × images), but at least 8 output rows per band where the LDS allows (the band's extra source rows,
       // ~2 at any scale, are read twice)
       const int ncol = (out_w + kColTile - 1) / kColTile;
-      const int cap = std::max(8, (out_h * cnt * ncol + 2047) / 2048);
+      int cap = std::max(8, (out_h * cnt * ncol + 2047) / 2048);
+      // a downscaled source's band stays near 24 source rows (a 4K → 1280² band of 25 output rows read ~47): the
+      // horizontal pass is a chain of row loads per thread, and the launch waits for its longest band
+      const double vscale = (double)im.height / out_h;
+      if (vscale > 1.0) cap = std::min(cap, std::max(4, (int)(24.0 / vscale)));
       if (T > cap) {
         T = cap;
         ntiles = (out_h + T - 1) / T;
@@ -400,6 +448,7 @@ extern "C" int sp_preprocess_u8(const sp_image_u8* images, int n, int out_h, int
       if (hc->ksize > max_ksh) max_ksh = hc->ksize;
     }
     const dim3 grid(max_tiles * ((out_w + kColTile - 1) / kColTile), cnt);
+    a.vec4 = out_w % 4 == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
     lds = (lds + 15) & ~15;
     if (max_ksh <= 3)  // up-scaling and same-size sources
       hipLaunchKernelGGL(preprocess_kernel<3>, grid, dim3(256), lds, s, a);

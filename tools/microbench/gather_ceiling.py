@@ -55,30 +55,30 @@ def main():
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.reps
 
-    for scale, B in ((1, 32), (1, 256), (2, 8)):
+    # (scale, B, bf16, ld): the bench configs' value_all layouts (C2 / C2-bf16: 6 decoder layers, ld 1536; C3 R18:
+    # 3 layers, ld 768; C5: 1280², bs8) and a compact ld-256 layout beside each
+    cases = [(1, 32, 0, 1536), (1, 32, 0, 256), (1, 32, 1, 1536), (1, 32, 1, 256), (1, 256, 1, 768),
+             (1, 256, 1, 256), (1, 256, 0, 768), (2, 8, 0, 1536), (2, 8, 0, 256), (2, 8, 1, 1536)]
+    for scale, B, bf16, ld in cases:
         S = 8400 * scale * scale
-        for bf16 in (0, 1):
-            esz = 2 if bf16 else 4
-            for ld in (1536, 256):
-                n = B * S * ld
-                if n * esz > 8 << 30:
-                    continue
-                val = torch.randn(n, device=dev)
-                if bf16:
-                    val = val.to(torch.bfloat16).view(torch.int16)
-                out = torch.empty(B * Q, device=dev)
-                gathered = B * Q * 8 * 12 * 4 * 32 * esz
-                for npt in (1, 4, 12):
-                    args = (bf16, npt, val.data_ptr(), ld, S, Q, B, scale, out.data_ptr(), st)
-                    assert L.gather_ceiling(*args) == 0
-                    ms = timed(lambda: L.gather_ceiling(*args))
-                    r = {"map": f"{80 * scale}^2+{40 * scale}^2+{20 * scale}^2", "B": B, "dtype": "bf16" if bf16 else "fp32",
-                         "ld": ld, "npt": npt, "slice_MB": round(B * S * 256 * esz / 1e6, 1), "ms": round(ms, 4),
-                         "gathered_MB": round(gathered / 1e6, 1), "gather_gbps": round(gathered / ms / 1e6, 1)}
-                    res.append(r)
-                    print(json.dumps(r), flush=True)
-                del val
-                torch.cuda.empty_cache()
+        esz = 2 if bf16 else 4
+        n = B * S * ld
+        val = torch.randn(n, device=dev)
+        if bf16:
+            val = val.to(torch.bfloat16).view(torch.int16)
+        out = torch.empty(B * Q, device=dev)
+        gathered = B * Q * 8 * 12 * 4 * 32 * esz
+        for npt in (1, 4, 12):
+            args = (bf16, npt, val.data_ptr(), ld, S, Q, B, scale, out.data_ptr(), st)
+            assert L.gather_ceiling(*args) == 0
+            ms = timed(lambda: L.gather_ceiling(*args))
+            r = {"map": f"{80 * scale}^2+{40 * scale}^2+{20 * scale}^2", "B": B, "dtype": "bf16" if bf16 else "fp32",
+                 "ld": ld, "npt": npt, "slice_MB": round(B * S * 256 * esz / 1e6, 1), "ms": round(ms, 4),
+                 "gathered_MB": round(gathered / 1e6, 1), "gather_gbps": round(gathered / ms / 1e6, 1)}
+            res.append(r)
+            print(json.dumps(r), flush=True)
+        del val
+        torch.cuda.empty_cache()
     # dense streaming read of a 275 MB / 1.1 GB buffer for comparison
     dense = []
     for mb in (275, 1100):

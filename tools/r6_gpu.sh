@@ -36,3 +36,21 @@ if [ "$PART" = bounds ]; then
   grep -v amdgpu.ids $OUT/served.log | cut -c1-240
   echo r6 bounds done
 fi
+if [ "$PART" = quick ]; then
+  SPOTTER_HIP_LIB=spotter_amd/_bounds/libspotter_bounds.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_kernels.py -q -k "bounds_build or gather_rows" --timeout 120 --timeout-method thread > $OUT/bounds_control.log 2>&1
+  tail -2 $OUT/bounds_control.log
+  timeout -k 10 300 python3 -u bench.py --size 1280 --batch 8 --stream mixed --no-cpu-baseline --latency-iters 0 --no-input-supply > $OUT/bench_c5mixed.log 2>&1
+  tail -1 $OUT/bench_c5mixed.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], json.dumps(d['kernel_classes']['preprocess']), json.dumps(d['kernel_classes']['msda']))"
+  timeout -k 10 300 python3 -u tools/microbench/gather_ceiling.py --out $OUT/gather_ceiling.json > $OUT/gather.log 2>&1
+  tail -1 $OUT/gather.log | cut -c1-600
+  echo r6 quick done
+fi
+if [ "$PART" = pre ]; then
+  timeout -k 10 300 python3 -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -q -k "preprocess or mixed_resolution" --timeout 200 --timeout-method thread > $OUT/pre_tests.log 2>&1
+  tail -1 $OUT/pre_tests.log
+  for i in 1 2; do
+    timeout -k 10 300 python3 -u bench.py --size 1280 --batch 8 --stream mixed --no-cpu-baseline --latency-iters 0 --no-input-supply > $OUT/bench_c5mixed_$i.log 2>&1
+    tail -1 $OUT/bench_c5mixed_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], json.dumps(d['kernel_classes']['preprocess']))"
+  done
+  echo r6 pre done
+fi
