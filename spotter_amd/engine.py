@@ -208,6 +208,9 @@ class Engine:
         # partial stores and the last workgroup's combine cost more than the reduce launch they replace,
         # profiles/r5/bs1/bs1_ab_splitk_combine.json), so off by default
         self.splitk_combine = splitk_combine
+        # linears over at most this many rows never split K (the bs1 decoder's 300-row GEMMs: one launch instead
+        # of partial + reduce); 0 = every launch may split (tools/bs1_ab.py "nosk<rows>" variants)
+        self.splitk_min_rows = 0
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -510,8 +513,9 @@ class Engine:
             ops.linear(x, rows, lw.k, lw.w, lw.n, tmp, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                        row_scale=row_scale, **self._splitk(), **_wkw(lw.w16))
             return ops.layernorm(tmp, *ln, out, rows, lw.n, self.cfg.layer_norm_eps)
+        sk = self._splitk() if rows > self.splitk_min_rows else {}
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
-                          row_scale=row_scale, **self._splitk(), **_wkw(lw.w16))
+                          row_scale=row_scale, **sk, **_wkw(lw.w16))
 
     C64_MIN_PIXELS = 1 << 18
     C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)

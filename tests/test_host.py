@@ -3,6 +3,7 @@ import os
 import pickle
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -847,6 +848,19 @@ def test_engine_refuses_fused_layernorm_on_bf16_linears():
     for prec in ("bf16", "bf16-all"):
         with pytest.raises(ValueError, match="fuse_ln"):
             Engine(PRESETS["r18vd"], {}, "cpu", precision=prec, fuse_ln=True)
+
+
+def test_served_sweep_coordinates_its_workers():
+    """tools/served_sweep.py's coordination on CPU (stub workers: a request is a 5 ms sleep): k processes report
+    ready, start on a common clock, count only requests finished inside the window, and the aggregate is the sum."""
+    sys.path.insert(0, ROOT)
+    from tools.served_sweep import sweep_point
+
+    r = sweep_point(3, "fp32", "r101vd", 1.0, 0, 60.0, stub_ms=5.0)
+    assert r["k_processes"] == 3 and len(r["per_process_img_per_s"]) == 3
+    assert 3 * 120 <= r["requests"] <= 3 * 200, r
+    assert abs(sum(r["per_process_img_per_s"]) - r["img_per_s"]) < 1.0
+    assert 5.0 <= r["p50_ms"] < 20.0
 
 
 def test_product_library_build_flags():

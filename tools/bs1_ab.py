@@ -60,6 +60,8 @@ def main():
         eng_run.WINO43_MIN_WORK = 1 << int(mode[1:]) if mode[:1] == "w" else Engine.WINO43_MIN_WORK
         eng_run.fuse_ln = mode == "ln"  # the post-LNs fused into the GEMM epilogue
         eng_run.splitk_combine = mode == "comb"  # "comb": split-K combined inside the GEMM launch
+        # "nosk<rows>": linears over at most <rows> rows never split K (Engine.splitk_min_rows)
+        eng_run.splitk_min_rows = int(mode[4:]) if mode.startswith("nosk") else 0
         ops.force_splitk_config(c, int(ms), int(mk))
         try:
             r = GraphRunner(eng_run, 1, cfg.image_size, cfg.image_size)

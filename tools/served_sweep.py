@@ -28,6 +28,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def stub_worker(ms: float):
+    """CPU test stand-in for worker(): the same READY / start / RESULT protocol, a request is a sleep of `ms`."""
+    print("READY", flush=True)
+    t_start, t_end = (float(v) for v in sys.stdin.readline().split())
+    while time.time() < t_start:
+        time.sleep(0.0005)
+    lat = []
+    while time.time() < t_end:
+        t0 = time.time()
+        time.sleep(ms / 1e3)
+        if time.time() <= t_end:
+            lat.append((time.time() - t0) * 1e3)
+    print("RESULT " + json.dumps({"pid": os.getpid(), "requests": len(lat), "lat_ms": [round(x, 3) for x in lat]}),
+          flush=True)
+
+
 def worker(preset: str, precision: str, warmup: int):
     import asyncio
 
@@ -76,13 +92,15 @@ def worker(preset: str, precision: str, warmup: int):
           flush=True)
 
 
-def sweep_point(k: int, precision: str, preset: str, seconds: float, warmup: int, timeout: float):
+def sweep_point(k: int, precision: str, preset: str, seconds: float, warmup: int, timeout: float,
+                stub_ms: float | None = None):
     import numpy as np
 
     env = dict(os.environ)
+    extra = ["--stub-ms", str(stub_ms)] if stub_ms is not None else []
     procs = [subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__), "--worker", "--preset", preset,
                                "--precision", precision,
-                               "--warmup", str(warmup)],
+                               "--warmup", str(warmup), *extra],
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT)
              for _ in range(k)]
     try:
@@ -132,8 +150,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--timeout", type=float, default=240.0, help="per sweep point: workers ready / finished")
     ap.add_argument("--out", default=None, help="directory for one JSON per precision")
+    ap.add_argument("--stub-ms", type=float, default=None, help=argparse.SUPPRESS)  # CPU test: no GPU worker
     a = ap.parse_args()
     if a.worker:
+        if a.stub_ms is not None:
+            return stub_worker(a.stub_ms)
         return worker(a.preset, a.precision[0], a.warmup)
     if max(a.k) > 12:
         raise SystemExit("at most 12 processes per GPU (the box allows 16 GPU processes in all)")
