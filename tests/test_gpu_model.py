@@ -316,6 +316,29 @@ def test_two_microbatch_streams_match_one():
         assert (sa - sb).abs().max() <= 1e-3
 
 
+def test_two_stream_forward_is_deterministic():
+    """Repeated Engine.forward(microbatches=2) calls give bit-identical logits and boxes: no kernel on the path
+    depends on what the other stream runs beside it. Round 6: the first point-sharing MSDA kernel, which exchanged
+    per-point records with cross-lane shuffles, gave a few wrong queries per launch here (never on a quiet GPU);
+    msda_h8l_kernel exchanges them through LDS (profiles/r6/msda/insitu_shuffle_exchange.log)."""
+    import torch
+
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+
+    g = np.load(os.path.join(GOLD, "r18vd_640.npz"))
+    model = SpotterForObjectDetection(PRESETS["r18vd"], use_graphs=False)
+    px = SpotterImageProcessor()(images=(load_images(g) * 64)[:16], return_tensors="pt")["pixel_values"].to("cuda")
+    eng = model.engine
+    outs = []
+    with torch.no_grad():
+        for _ in range(8):
+            outs.append([t.clone() for t in eng.forward(px, microbatches=2)])
+    torch.cuda.synchronize()
+    for lg, bx in outs[1:]:
+        assert torch.equal(lg, outs[0][0]) and torch.equal(bx, outs[0][1])
+
+
 def test_batch_equals_single(tmp_path):
     """bs=3 in one engine call gives the same per-image outputs as three bs=1 calls (bs1 GEMMs use
     split-K, so the fp32 summation order differs: compare at the parity bar, not bitwise)."""

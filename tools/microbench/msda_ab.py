@@ -1,6 +1,7 @@
-"""sp_msda at the bench configs' decoder shapes, both kernels (msda_h8_kernel, and msda_vec_kernel via
-sp_set_tuning(SP_TUNE_MSDA_GENERIC, 1)) alternating in one process: per-launch time, gathered-corner rate and
-bit-identity of the outputs. Sampling offsets / logits are random (offsets × 2, like a trained decoder's spread).
+"""sp_msda at the bench configs' decoder shapes, both kernels for the decoder's shape alternating in one process
+(sp_set_tuning(SP_TUNE_MSDA_GENERIC, v): 0 msda_h8l_kernel, the default; 1 msda_vec_kernel): per-launch time,
+gathered-corner rate and bit-identity of the outputs against msda_vec_kernel. (Round 6's first measurement also
+carried v = 2, the since-removed shuffle-exchange kernel: profiles/r6/msda/msda_ab.json.) Sampling offsets / logits are random (offsets × 2, like a trained decoder's spread).
 
     python tools/microbench/msda_ab.py [--reps 50] [--out profiles/r6/msda/msda_ab.json]
 """
@@ -55,7 +56,8 @@ def main():
             ops.msda(value, 2 * D, V(offaw.view(-1), 0, offaw.shape[1]), ref, V(out, 0, D), B, S, Q, nH, dh, shapes,
                      starts, nP, 0.5)
 
-        times = {0: [], 1: []}
+        names = {0: "h8l", 1: "vec"}
+        times = {g: [] for g in names}
         outs = {}
         for rnd in range(6):
             for g in (1, 0) if rnd % 2 else (0, 1):
@@ -72,12 +74,16 @@ def main():
                 times[g].append(e0.elapsed_time(e1) / a.reps)
                 outs[g] = out.clone()
         L.sp_set_tuning(4, 0)
-        ms_new, ms_old = float(np.median(times[0])), float(np.median(times[1]))
-        res[name] = {"B": B, "size": size, "bf16": bf16, "ms_h8": round(ms_new, 4), "ms_vec": round(ms_old, 4),
-                     "speedup": round(ms_old / ms_new, 3), "gather_gbps_h8": round(gathered / ms_new / 1e6, 1),
-                     "gather_gbps_vec": round(gathered / ms_old / 1e6, 1),
-                     "bit_identical": bool(torch.equal(outs[0], outs[1])),
-                     "max_rel_diff": float((outs[0] - outs[1]).abs().max() / outs[1].abs().max())}
+        ms = {g: float(np.median(times[g])) for g in names}
+        r = {"B": B, "size": size, "bf16": bf16}
+        for g, nm in names.items():
+            r[f"ms_{nm}"] = round(ms[g], 4)
+            r[f"gather_gbps_{nm}"] = round(gathered / ms[g] / 1e6, 1)
+            if g != 1:
+                r[f"speedup_{nm}_vs_vec"] = round(ms[1] / ms[g], 3)
+                r[f"bit_identical_{nm}"] = bool(torch.equal(outs[g], outs[1]))
+                r[f"max_rel_diff_{nm}"] = float((outs[g] - outs[1]).abs().max() / outs[1].abs().max())
+        res[name] = r
         print(json.dumps({name: res[name]}), flush=True)
     if a.out:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
