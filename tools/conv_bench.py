@@ -54,6 +54,14 @@ SHAPES = [
     (256, 160, 160, 64, 64, 3, 1, "relu", False, 4),    # 29 stage0 3x3
     (256, 40, 40, 256, 256, 3, 1, "relu", False, 3),    # 30 stage2 3x3
     (1, 1, 2150400, 256, 768, 1, 1, None, False, 1),    # 31 C3 decoder value_all (3 layers x 256)
+    # C3 decoder linears (bs256 x 300 queries; fp32 rows, bf16 weights) and the encoder output head
+    (1, 1, 76800, 256, 256, 1, 1, None, False, 11),     # 32 dec 256->256 (v, o, bbox)
+    (1, 1, 76800, 256, 512, 1, 1, None, False, 3),      # 33 dec qk (256->512)
+    (1, 1, 76800, 256, 1024, 1, 1, "relu", False, 3),   # 34 dec fc1
+    (1, 1, 76800, 1024, 256, 1, 1, None, True, 3),      # 35 dec fc2 (+res)
+    (1, 1, 76800, 256, 288, 1, 1, None, False, 3),      # 36 dec offsets/weights
+    (1, 1, 2150400, 256, 256, 1, 1, None, False, 1),    # 37 C3 enc_output
+    (1, 1, 2150400, 256, 80, 1, 1, None, False, 1),     # 38 C3 enc_score
 ]
 
 
