@@ -7,7 +7,7 @@
  *   processor(images=PIL, return_tensors="pt")           -> sp_preprocess_u8
  *   model(**inputs) (RTDetrV2ForObjectDetection.forward) -> sp_conv2d, sp_maxpool3x3s2,
  *        sp_avgpool2x2_ceil, sp_upsample2x_nearest, sp_layernorm, sp_attention,
- *        sp_msda, sp_rowmax, sp_topk_rows, sp_gather_rows, sp_ref_init, sp_box_refine
+ *        sp_msda, sp_rowmax, sp_topk_rows, sp_gather_rows, sp_add_rows, sp_ref_init, sp_box_refine
  *   processor.post_process_object_detection(...)         -> sp_postprocess
  * (HF sources: transformers/models/rt_detr/image_processing_pil_rt_detr.py:
  * 451-462, 508-578; transformers/models/rt_detr_v2/modeling_rt_detr_v2.py:
@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define SP_ABI_VERSION 14
+#define SP_ABI_VERSION 15
 
 enum sp_act { SP_ACT_NONE = 0, SP_ACT_RELU = 1, SP_ACT_SILU = 2, SP_ACT_GELU = 3 };
 /* GEMM operand precision:
@@ -272,6 +272,12 @@ int sp_rowmax(const float* x, int64_t ldx, int64_t rows, int c, float* out, void
 /* dst[b, i, :] = src[b*src_rows + idx[b, i], :] */
 int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,
                    int batch, int d, float* dst, int64_t ld_dst, void* stream);
+/* ABI v15. y[r, 0:cols] = a[r, :] + b[r, :] in fp32, written as fp32 rows (y) or rounded RNE to bf16 rows
+ * (y_bf16; exactly one of the two): the decoder / AIFI attention input h + pos (M2:395-404, M2:409-423),
+ * materialised so the q/k and offset projections load it by LDS-DMA instead of adding it in a register-staged
+ * loader (sp_conv_desc.A2). cols % 8 == 0, lda / ldb % 4 == 0, ldy % 8 == 0, 16-byte aligned rows. */
+int sp_add_rows(const float* a, int64_t lda, const float* b, int64_t ldb, float* y, uint16_t* y_bf16, int64_t ldy,
+                int rows, int cols, void* stream);
 /* ref[b,i,:] = sigmoid(delta[b,i,:] + anchors[idx[b,i],:]) (M2:1597-1603, M2:616). */
 int sp_ref_init(const float* delta, int64_t ld_delta, const float* anchors, const int32_t* idx,
                 int batch, int k, float* ref, void* stream);

@@ -13,7 +13,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPOTTER_HIP_LIB", os.path.join(HERE, "libspotter_hip.so"))
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 vp = C.c_void_p
 i32 = C.c_int32
@@ -124,6 +124,7 @@ _SIGS = {
     "sp_gather_rows": (i32, [vp, i64, i32, vp, i32, i32, i32, vp, i64, vp]),
     "sp_ref_init": (i32, [vp, i64, vp, vp, i32, i32, vp, vp]),
     "sp_box_refine": (i32, [vp, i64, vp, i32, vp]),
+    "sp_add_rows": (i32, [vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
     "sp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp]),
     "sp_jpeg_decode_coefs": (i32, [vp, i64, C.POINTER(SpJpegLayout), vp, i64]),
     "sp_jpeg_to_rgb": (i32, [vp, C.POINTER(SpJpegLayout), vp, i64, vp, i64, vp, vp]),

@@ -366,6 +366,35 @@ __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src
   }
 }
 
+// y = a + b over `rows` rows of 8·c8 columns (fp32 in), stored as fp32 rows or rounded RNE to bf16 rows: the
+// attention input q = k = h + pos (M2:395-404 / 409-423) materialised once so that the query / offset
+// projections take their A operand by LDS-DMA. The bf16 form is the operand the bf16-mode GEMM would have
+// rounded in its own loader (v_cvt_pk_bf16_f32 of the same fp32 sum), so the products are unchanged.
+__global__ __launch_bounds__(256) void add_rows_kernel(const float* __restrict__ a, int64_t lda,
+                                                       const float* __restrict__ b, int64_t ldb,
+                                                       float* __restrict__ y, uint16_t* __restrict__ y16,
+                                                       int64_t ldy, int rows, int c8) {
+  const int64_t total = (int64_t)rows * c8;
+  for (int64_t i = gtid(); i < total; i += grid_stride()) {
+    const int64_t r = i / c8;
+    const int q = (int)(i - r * c8) * 8;
+    SP_BCHECK(q + 7, lda < ldb ? lda : ldb);
+    SP_BCHECK(q + 7, ldy);
+    const float4* pa = reinterpret_cast<const float4*>(a + r * lda + q);
+    const float4* pb = reinterpret_cast<const float4*>(b + r * ldb + q);
+    const float4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    const float f[8] = {a0.x + b0.x, a0.y + b0.y, a0.z + b0.z, a0.w + b0.w,
+                        a1.x + b1.x, a1.y + b1.y, a1.z + b1.z, a1.w + b1.w};
+    if (y16) {
+      *reinterpret_cast<uint4*>(y16 + r * ldy + q) = pack8(f);
+    } else {
+      float4* py = reinterpret_cast<float4*>(y + r * ldy + q);
+      py[0] = make_float4(f[0], f[1], f[2], f[3]);
+      py[1] = make_float4(f[4], f[5], f[6], f[7]);
+    }
+  }
+}
+
 __global__ void ref_init_kernel(const float* __restrict__ delta, int64_t ld, const float* __restrict__ anchors,
                                 const int32_t* __restrict__ idx, int batch, int k,
                                 float* __restrict__ ref) {
@@ -508,6 +537,19 @@ extern "C" int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, co
   hipLaunchKernelGGL(gather_rows_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), src,
                      ld_src, src_rows, idx, k, batch, d, dst, ld_dst);
   return check_launch("sp_gather_rows");
+}
+
+extern "C" int sp_add_rows(const float* a, int64_t lda, const float* b, int64_t ldb, float* y, uint16_t* y_bf16,
+                           int64_t ldy, int rows, int cols, void* stream) {
+  SP_ARG_CHECK(a && b && (y != nullptr) != (y_bf16 != nullptr) && rows > 0 && cols > 0,
+               "sp_add_rows: bad args (exactly one of y / y_bf16)");
+  const uintptr_t al = (uintptr_t)a | (uintptr_t)b | (uintptr_t)(y ? (const void*)y : (const void*)y_bf16);
+  SP_ARG_CHECK(cols % 8 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldy % 8 == 0 && lda >= cols && ldb >= cols &&
+                   ldy >= cols && (al & 15) == 0,
+               "sp_add_rows: cols %% 8, lda / ldb %% 4, ldy %% 8 and 16-byte aligned rows required");
+  hipLaunchKernelGGL(add_rows_kernel, dim3(grid_for((int64_t)rows * (cols / 8))), dim3(256), 0, as_stream(stream),
+                     a, lda, b, ldb, y, y_bf16, ldy, rows, cols / 8);
+  return check_launch("sp_add_rows");
 }
 
 extern "C" int sp_ref_init(const float* delta, int64_t ld_delta, const float* anchors, const int32_t* idx,

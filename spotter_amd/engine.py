@@ -211,6 +211,8 @@ class Engine:
         # linears over at most this many rows never split K (the bs1 decoder's 300-row GEMMs: one launch instead
         # of partial + reduce); 0 = every launch may split (tools/bs1_ab.py "nosk<rows>" variants)
         self.splitk_min_rows = 0
+        # the h + pos attention inputs materialised for the LDS-DMA tiles (_lin_plus); False = the A2 addend (A/B)
+        self.add_rows = True
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -517,6 +519,20 @@ class Engine:
         return ops.linear(x, rows, lw.k, lw.w, lw.n, out, bias=lw.b, act=act, res1=res1, res2=res2, a2=a2,
                           row_scale=row_scale, **sk, **_wkw(lw.w16))
 
+    def _lin_plus(self, x: V, addend: V | None, rows, lw: LinW, out: V, key: str):
+        """out = (x + addend) @ W + b: the attention projections whose input is h + pos (M2:395-404, 409-423; AIFI
+        M2:873-880). On the bf16 / split kernels the sum is materialised once (sp_add_rows; bf16 rows in the bf16
+        mode, the operand that kernel's loader would have rounded) so the GEMM loads it by LDS-DMA; their A2
+        addend exists only in the register-staged tiles, 2.7x slower on C3's decoder projections
+        (profiles/r6/c3tail/). The fp32 MFMA kernel keeps its in-loader add."""
+        if addend is None:
+            return self._lin_op(x, rows, lw, out)
+        if not self.add_rows or lw.mode == "f32":
+            return self._lin_op(x, rows, lw, out, a2=addend)
+        hp = view(self._buf(key, rows, lw.k, dtype=torch.int16 if lw.mode == "bf16" else torch.float32), lw.k)
+        ops.add_rows(x, addend, hp, rows, lw.k)
+        return self._lin_op(hp, rows, lw, out)
+
     C64_MIN_PIXELS = 1 << 18
     C32_MIN_PIXELS = 1 << 19  # sp_conv3x3_c32 from about 4 tiles per CU up (bs8 at 320²: 1.08-1.17x)
 
@@ -685,7 +701,8 @@ class Engine:
         ff = self._buf("aifi_ff", rows, cfg.encoder_ffn_dim)
         p5a = self._buf("p5a", rows, Hd)
         # with config.eval_size set HF runs AIFI without the position embedding (M2:1073-1081)
-        self._lin_op(view(p5, Hd), rows, A["qk"], view(qk, 2 * Hd), a2=None if cfg.eval_size else view(pos, Hd))
+        self._lin_plus(view(p5, Hd), None if cfg.eval_size else view(pos, Hd), rows, A["qk"], view(qk, 2 * Hd),
+                       "aifi_hp")
         self._lin_op(view(p5, Hd), rows, A["v"], view(vv, Hd))
         heads = cfg.encoder_attention_heads
         ops.attention(V(qk, 0, 2 * Hd), V(qk, Hd, 2 * Hd), view(vv, Hd), view(at, Hd), B, n, heads, Hd // heads,
@@ -880,13 +897,13 @@ class Engine:
             self._lin_op(view(ref, 4), Bq, self.qpos[0], view(qp, 2 * D), act="relu")
             self._lin_op(view(qp, 2 * D), Bq, self.qpos[1], view(pos, D))
             # self-attention, q = k = h + pos, v = h (M2:395-404)
-            self._lin_op(view(h, D), Bq, P["qk"], view(qk, 2 * D), a2=view(pos, D))
+            self._lin_plus(view(h, D), view(pos, D), Bq, P["qk"], view(qk, 2 * D), "dec_hp")
             self._lin_op(view(h, D), Bq, P["v"], view(vv, D))
             ops.attention(V(qk, 0, 2 * D), V(qk, D, 2 * D), view(vv, D), view(at, D), B, Q, nH, D // nH,
                           (D // nH) ** -0.5, bf16=self._attn_bf16)
             self._lin_op(view(at, D), Bq, P["o"], view(h, D), res1=view(h, D), ln=P["ln1"])  # in place: row-local
             # deformable cross-attention (M2:409-423)
-            self._lin_op(view(h, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), a2=view(pos, D))
+            self._lin_plus(view(h, D), view(pos, D), Bq, P["offaw"], view(offaw, nH * nL * nP * 3), "dec_hp")
             ops.msda(V(vall, 0, L * D), j * D, view(offaw, nH * nL * nP * 3), ref, view(at, D), B, S, Q, nH,
                      D // nH, shapes, starts, nP, cfg.decoder_offset_scale)
             self._lin_op(view(at, D), Bq, P["out"], view(h, D), res1=view(h, D), ln=P["ln2"])

@@ -513,6 +513,18 @@ def gather_rows(src: V, src_rows, idx: torch.Tensor, k, batch, d, dst: V):
                                               stream()), 0, 4 * batch * k * (2 * d + 1))
 
 
+def add_rows(a: V, b: V, out: V, rows: int, cols: int):
+    """out = a + b (fp32 rows in; out fp32 rows, or bf16 rows rounded RNE when out holds int16 patterns)."""
+    ap = a.need(rows, cols, "add_rows.a")
+    bp = b.need(rows, cols, "add_rows.b")
+    if out.is_bf16:
+        yp, y16 = None, out.need(rows, cols, "add_rows.out", bf16=True)
+    else:
+        yp, y16 = out.need(rows, cols, "add_rows.out"), None
+    _launch("elementwise", "sp_add_rows", (ap, a.ld, bp, b.ld, yp, y16, out.ld, rows, cols, stream()), 0,
+            rows * cols * (8 + out.t.element_size()))
+
+
 def ref_init(delta: V, anchors: torch.Tensor, idx: torch.Tensor, batch, k, ref: torch.Tensor):
     dp = delta.need(batch * k, 4, "ref_init.delta")
     assert ref.numel() >= batch * k * 4

@@ -1257,3 +1257,25 @@ def test_bounds_build_reports_a_violation(dev):
     assert "elementwise.hip" in rep and f"index={src_rows} extent={src_rows}" in rep, rep
     assert L.sp_bounds_report(buf, len(buf)) == 0  # reset
     np.testing.assert_array_equal(dst.view(2 * k, d)[2].cpu().numpy(), src.view(-1, d)[src_rows].cpu().numpy())
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_add_rows(dev, bf16):
+    """sp_add_rows (the h + pos attention input): fp32 sums bit-exact; the bf16 form equals the fp32 sum rounded
+    RNE (the numpy oracle's bf16_bits, the same rounding the bf16 GEMM loader applies), on strided rows."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V, bf16_bits
+
+    rng = np.random.default_rng(seed(("add_rows", bf16)))
+    rows, cols, lda, ldb, ldy = 300, 256, 260, 512, 264
+    a = rng.standard_normal((rows, lda)).astype(np.float32)
+    b = (rng.standard_normal((rows, ldb)) * 3.0).astype(np.float32)
+    want = a[:, :cols] + b[:, :cols]
+    out = torch.zeros(rows * ldy, device=dev, dtype=torch.int16 if bf16 else torch.float32)
+    ops.add_rows(V(T(a.reshape(-1), dev), 0, lda), V(T(b.reshape(-1), dev), 0, ldb), V(out, 0, ldy), rows, cols)
+    got = out.cpu().numpy().reshape(rows, ldy)
+    if bf16:
+        assert np.array_equal(got[:, :cols].view(np.uint16), bf16_bits(want).reshape(rows, cols))
+    else:
+        assert np.array_equal(got[:, :cols], want)
+    assert not got[:, cols:].any()  # nothing written past the row
