@@ -250,6 +250,10 @@ int sp_upsample2x_nearest(const float* x, int64_t ldx, float* y, int64_t ldy, in
 /* nn.LayerNorm over the last dim (d <= 1024). */
 int sp_layernorm(const float* x, int64_t ldx, const float* gamma, const float* beta, float* y,
                  int64_t ldy, int rows, int d, float eps, void* stream);
+/* ABI v15. sp_layernorm at d = 256 with the output rounded RNE to bf16 rows: the bf16 variant's encoder head,
+ * whose score projection rounds its operand to bf16 anyway (M2:1587-1593). */
+int sp_layernorm_bf16(const float* x, int64_t ldx, const float* gamma, const float* beta, uint16_t* y, int64_t ldy,
+                      int rows, int d, float eps, void* stream);
 /* softmax(Q Kᵀ · scale) V per (batch, head); Q/K/V rows [batch*n, ld], head h at col h*dh. */
 int sp_attention(const float* q, int64_t ldq, const float* k, int64_t ldk, const float* v,
                  int64_t ldv, float* o, int64_t ldo, int batch, int n, int heads, int dh,

@@ -116,6 +116,7 @@ _SIGS = {
     "sp_conv3x3_c64_bf16": (i32, [vp, i64, vp, vp, vp, vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_upsample2x_nearest": (i32, [vp, i64, vp, i64, i32, i32, i32, i32, vp]),
     "sp_layernorm": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),
+    "sp_layernorm_bf16": (i32, [vp, i64, vp, vp, vp, i64, i32, i32, f32, vp]),
     "sp_attention": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),
     "sp_attention_bf16": (i32, [vp, i64, vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, f32, vp]),
     "sp_msda": (i32, [C.POINTER(SpMsdaDesc), vp]),

@@ -312,11 +312,14 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
+// y16 (instead of y): the normalised row rounded RNE to bf16 (sp_layernorm_bf16), for a consumer that rounds its
+// operand to bf16 anyway (the bf16 variant's encoder score head). One instantiation for both stores, so the row
+// arithmetic is compiled once: the bf16 rows are exactly the fp32 rows rounded.
 __global__ __launch_bounds__(256) void layernorm256_kernel(const float* __restrict__ x, int64_t ldx,
                                                            const float* __restrict__ g,
                                                            const float* __restrict__ b,
-                                                           float* __restrict__ y, int64_t ldy, int rows,
-                                                           float eps) {
+                                                           float* __restrict__ y, uint16_t* __restrict__ y16,
+                                                           int64_t ldy, int rows, float eps) {
   const int lane = threadIdx.x & 63, l16 = lane & 15;
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
   const float4* g4 = reinterpret_cast<const float4*>(g);
@@ -345,11 +348,15 @@ __global__ __launch_bounds__(256) void layernorm256_kernel(const float* __restri
   }
   const float var = group16_sum(q) * (1.0f / 256.0f);
   const float rstd = 1.0f / sqrtf(var + eps);
-  float4* yr = reinterpret_cast<float4*>(y + row * ldy);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    yr[l16 + 16 * i] = make_float4((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y,
-                                   (v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
+  for (int i = 0; i < 4; ++i) {
+    const float4 o = make_float4((v[i].x - mean) * rstd * gg[i].x + bb[i].x, (v[i].y - mean) * rstd * gg[i].y + bb[i].y,
+                                 (v[i].z - mean) * rstd * gg[i].z + bb[i].z, (v[i].w - mean) * rstd * gg[i].w + bb[i].w);
+    if (y16)
+      reinterpret_cast<uint2*>(y16 + row * ldy)[l16 + 16 * i] = make_uint2(pk_bf16(o.x, o.y), pk_bf16(o.z, o.w));
+    else
+      reinterpret_cast<float4*>(y + row * ldy)[l16 + 16 * i] = o;
+  }
 }
 
 __global__ void gather_rows_kernel(const float* __restrict__ src, int64_t ld_src, int src_rows,
@@ -523,11 +530,21 @@ extern "C" int sp_layernorm(const float* x, int64_t ldx, const float* gamma, con
                   (((uintptr_t)x | (uintptr_t)y | (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0;
   if (vec && d == 256)
     hipLaunchKernelGGL(layernorm256_kernel, dim3((rows + 15) / 16), dim3(256), 0, as_stream(stream), x, ldx, gamma,
-                       beta, y, ldy, rows, eps);
+                       beta, y, nullptr, ldy, rows, eps);
   else
     hipLaunchKernelGGL(vec ? layernorm4_kernel : layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0,
                        as_stream(stream), x, ldx, gamma, beta, y, ldy, rows, d, eps);
   return check_launch("sp_layernorm");
+}
+
+extern "C" int sp_layernorm_bf16(const float* x, int64_t ldx, const float* gamma, const float* beta, uint16_t* y,
+                                 int64_t ldy, int rows, int d, float eps, void* stream) {
+  SP_ARG_CHECK(x && gamma && beta && y && rows > 0 && d == 256 && ldx % 4 == 0 && ldy % 4 == 0 &&
+                   (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) == 0 && ((uintptr_t)y & 7) == 0,
+               "sp_layernorm_bf16: d = 256, ldx / ldy %% 4, 16-byte aligned fp32 rows, 8-byte aligned bf16 rows");
+  hipLaunchKernelGGL(layernorm256_kernel, dim3((rows + 15) / 16), dim3(256), 0, as_stream(stream), x, ldx, gamma,
+                     beta, nullptr, y, ldy, rows, eps);
+  return check_launch("sp_layernorm_bf16");
 }
 
 extern "C" int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,

@@ -213,6 +213,9 @@ class Engine:
         self.splitk_min_rows = 0
         # the h + pos attention inputs materialised for the LDS-DMA tiles (_lin_plus); False = the A2 addend (A/B)
         self.add_rows = True
+        # the bf16 variant's encoder head LayerNorm written as bf16 rows for the score projection (decode); False =
+        # the fp32 normalised map (A/B)
+        self.enc_head_bf16 = True
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -859,17 +862,36 @@ class Engine:
         anchors, valid = self._const(("anchors", tuple(shapes)), lambda: tuple(
             _t(a, self.dev) for a in anchors_for(shapes)))
         rows = B * S
-        om = self._buf("om", rows, D)
         cls = self._buf("enc_cls", rows, NC)
-        self._lin_op(view(src, D), rows, self.enc_output, view(om, D), row_scale=valid, ln=self.enc_ln)
-        self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
+        lw = self.enc_output
+        # the bf16 variant's score projection rounds its operand to bf16 anyway: the encoder head's LayerNorm
+        # writes bf16 rows for it (half the write and the read of the normalised map), and the Q selected rows
+        # per image are normalised again from the pre-norm rows for the decoder (LayerNorm is row-local: the
+        # same kernel on the same row gives the same bits as gathering the fp32 normalised map)
+        bf16_head = self.enc_head_bf16 and self.enc_score.mode == "bf16" and not self.fuse_ln and D == 256
+        if bf16_head:
+            pre = view(self._buf("ln_tmp", rows, lw.n), lw.n)
+            ops.linear(view(src, D), rows, lw.k, lw.w, lw.n, pre, bias=lw.b, row_scale=valid, **self._splitk(),
+                       **_wkw(lw.w16))
+            om16 = self._buf("om16", rows, D, dtype=torch.int16)
+            ops.layernorm(pre, *self.enc_ln, view(om16, D), rows, D, cfg.layer_norm_eps)
+            self._lin_op(view(om16, D), rows, self.enc_score, view(cls, NC))
+        else:
+            om = self._buf("om", rows, D)
+            self._lin_op(view(src, D), rows, lw, view(om, D), row_scale=valid, ln=self.enc_ln)
+            self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
         topk = self._buf("topk", B, Q, dtype=torch.int32)
         cmax = self._buf("enc_cls_max", rows)
         ops.rowmax(view(cls, NC), rows, NC, cmax)
         ops.topk_rows(V(cmax, 0, S), B, S, Q, topk)
         Bq = B * Q
         h = self._buf("dec_h", Bq, D)
-        ops.gather_rows(view(om, D), S, topk, Q, B, D, view(h, D))
+        if bf16_head:
+            hraw = self._buf("dec_hraw", Bq, D)
+            ops.gather_rows(pre, S, topk, Q, B, D, view(hraw, D))
+            ops.layernorm(view(hraw, D), *self.enc_ln, view(h, D), Bq, D, cfg.layer_norm_eps)
+        else:
+            ops.gather_rows(view(om, D), S, topk, Q, B, D, view(h, D))
         t_a = self._buf("dec_ta", Bq, D)
         t_b = self._buf("dec_tb", Bq, D)
         delta = self._buf("dec_delta", Bq, 4)

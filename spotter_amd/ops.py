@@ -440,10 +440,12 @@ def upsample2x(x: V, y: V, n, h, w, c):
 
 
 def layernorm(x: V, gamma, beta, y: V, rows, d, eps=1e-5):
+    """y = LayerNorm(x) over d; y may hold bf16 rows (int16 patterns; d = 256 only): rounded RNE at the store."""
     xp = x.need(rows, d, "ln.x")
-    yp = y.need(rows, d, "ln.y")
-    _launch("layernorm", "sp_layernorm", (xp, x.ld, gamma.data_ptr(), beta.data_ptr(), yp, y.ld, rows, d, eps,
-                                           stream()), 8 * rows * d, 8 * rows * d)
+    yp = y.need(rows, d, "ln.y", bf16=y.is_bf16)
+    _launch("layernorm", "sp_layernorm_bf16" if y.is_bf16 else "sp_layernorm",
+            (xp, x.ld, gamma.data_ptr(), beta.data_ptr(), yp, y.ld, rows, d, eps, stream()), 8 * rows * d,
+            (4 + y.t.element_size()) * rows * d)
 
 
 def attention(q: V, k: V, v: V, o: V, batch, n, heads, dh, scale, bf16: bool = False):

@@ -885,6 +885,39 @@ def test_layernorm_256_rows_views(dev):
         assert np.all(got[:, 256:] == 7.0)
 
 
+def test_layernorm_bf16_rows(dev):
+    """sp_layernorm_bf16 (ABI v15, the bf16 variant's encoder head): the fp32 kernel's rows rounded RNE to bf16,
+    bit for bit, on ragged row counts and strided views; and LayerNorm is row-local, so normalising gathered rows
+    equals gathering normalised rows (what Engine.decode relies on for the decoder's initial queries)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V, bf16_bits
+
+    rng = np.random.default_rng(55)
+    g = T(rng.uniform(0.5, 1.5, 256).astype(np.float32), dev)
+    b = T(rng.standard_normal(256).astype(np.float32), dev)
+    for rows in (1, 15, 17, 1001):
+        x = T((rng.standard_normal((rows, 320)) * 2 - 1).astype(np.float32).reshape(-1), dev)
+        y32 = torch.empty(rows * 256, device=dev)
+        ops.layernorm(V(x, 32, 320), g, b, V(y32, 0, 256), rows, 256)
+        y16 = torch.full((rows * 264,), 7, dtype=torch.int16, device=dev)
+        ops.layernorm(V(x, 32, 320), g, b, V(y16, 0, 264), rows, 256)
+        got = y16.cpu().numpy().reshape(rows, 264)
+        assert np.array_equal(got[:, :256].view(np.uint16), bf16_bits(y32.cpu().numpy()).reshape(rows, 256))
+        assert np.all(got[:, 256:] == 7)
+    rows, k = 1000, 300
+    x = T(rng.standard_normal((rows, 256)).astype(np.float32).reshape(-1), dev)
+    idx = T(rng.permutation(rows)[:k].astype(np.int32), dev)
+    full = torch.empty(rows * 256, device=dev)
+    ops.layernorm(V(x, 0, 256), g, b, V(full, 0, 256), rows, 256)
+    a = torch.empty(k * 256, device=dev)
+    ops.gather_rows(V(full, 0, 256), rows, idx, k, 1, 256, V(a, 0, 256))
+    raw = torch.empty(k * 256, device=dev)
+    ops.gather_rows(V(x, 0, 256), rows, idx, k, 1, 256, V(raw, 0, 256))
+    b2 = torch.empty(k * 256, device=dev)
+    ops.layernorm(V(raw, 0, 256), g, b, V(b2, 0, 256), k, 256)
+    assert torch.equal(a, b2)
+
+
 @pytest.mark.parametrize("d", [256, 258, 384, 1000])  # 258: scalar path, 256: four rows per wave, others: float4
 def test_layernorm(dev, d):
     from spotter_amd import ops

@@ -1,8 +1,9 @@
-"""Same-process A/B of Engine.add_rows (the h + pos attention inputs materialised by sp_add_rows so the q/k and
-offset projections take the LDS-DMA tiles) against the register-staged A2 addend, alternating on one engine per
-config: ms per forward (HIP events over `iters` eager forwards) and the max |Δ| of the outputs.
+"""Same-process A/B of an Engine knob, alternating on one engine per config: ms per forward (HIP events over
+`iters` eager forwards) and the max |Δ| of the outputs. --knob add_rows (default): the h + pos attention inputs
+materialised by sp_add_rows so the q/k and offset projections take the LDS-DMA tiles, against the register-staged
+A2 addend; --knob enc_head_bf16: the bf16 variant's encoder-head LayerNorm into bf16 rows, against the fp32 map.
 
-    python tools/add_rows_ab.py [--configs c3,c2bf16,c2] [--iters 10] [--rounds 3] [--out f.json]
+    python tools/engine_knob_ab.py [--knob add_rows] [--configs c3,c2bf16,c2] [--iters 10] [--rounds 3] [--out f.json]
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ CONFIGS = {"c3": ("r18vd", "bf16", 256), "c2bf16": ("r101vd", "bf16", 32), "c2":
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--knob", default="add_rows")
     ap.add_argument("--configs", default="c3,c2bf16,c2")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
@@ -39,7 +41,7 @@ def main():
         times = {True: [], False: []}
         for r in range(a.rounds):
             for mode in ((True, False) if r % 2 == 0 else (False, True)):
-                eng.add_rows = mode
+                setattr(eng, a.knob, mode)
                 with torch.no_grad():
                     for _ in range(2):
                         eng.forward(px)
@@ -52,13 +54,13 @@ def main():
                     torch.cuda.synchronize()
                 times[mode].append(e0.elapsed_time(e1) / a.iters)
                 outs[mode] = (lg.clone(), bx.clone())
-        eng.add_rows = True
+        setattr(eng, a.knob, True)
         dl = float((outs[True][0] - outs[False][0]).abs().max())
         db = float((outs[True][1] - outs[False][1]).abs().max())
-        e = {"config": name, "ms_add_rows": sorted(times[True])[len(times[True]) // 2],
-             "ms_a2": sorted(times[False])[len(times[False]) // 2], "runs_add_rows": times[True],
-             "runs_a2": times[False], "max_dlogit": dl, "max_dbox": db}
-        e["speedup"] = round(e["ms_a2"] / e["ms_add_rows"], 4)
+        e = {"config": name, "knob": a.knob, "ms_on": sorted(times[True])[len(times[True]) // 2],
+             "ms_off": sorted(times[False])[len(times[False]) // 2], "runs_on": times[True],
+             "runs_off": times[False], "max_dlogit": dl, "max_dbox": db}
+        e["speedup"] = round(e["ms_off"] / e["ms_on"], 4)
         res.append(e)
         print(json.dumps(e), flush=True)
         del model, eng, px, outs
