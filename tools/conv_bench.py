@@ -62,6 +62,7 @@ SHAPES = [
     (1, 1, 76800, 256, 288, 1, 1, None, False, 3),      # 36 dec offsets/weights
     (1, 1, 2150400, 256, 256, 1, 1, None, False, 1),    # 37 C3 enc_output
     (1, 1, 2150400, 256, 80, 1, 1, None, False, 1),     # 38 C3 enc_score
+    (256, 80, 80, 128, 256, 1, 1, None, False, 2),      # 39 C3 CCFM 1x1 128->256 @80² (short K)
 ]
 
 
