@@ -339,6 +339,32 @@ def test_two_stream_forward_is_deterministic():
         assert torch.equal(lg, outs[0][0]) and torch.equal(bx, outs[0][1])
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_operand_materialisations_are_bit_identical(precision):
+    """Engine.add_rows (h + pos materialised by sp_add_rows for the LDS-DMA tiles) and Engine.enc_head_bf16 (the
+    bf16 variant's encoder-head LayerNorm into bf16 rows, decoder queries normalised from the gathered pre-norm
+    rows) change where operands are rounded or added, not their values: the logits and boxes equal the A2-addend /
+    fp32-map forms bit for bit (round 6)."""
+    import torch
+
+    from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
+    from spotter_amd.config import PRESETS
+
+    g = np.load(os.path.join(GOLD, "r18vd_640.npz"))
+    model = SpotterForObjectDetection(PRESETS["r18vd"], use_graphs=False, precision=precision)
+    px = SpotterImageProcessor()(images=(load_images(g) * 8)[:16], return_tensors="pt")["pixel_values"].to("cuda")
+    eng = model.engine
+    outs = {}
+    for knobs in ((True, True), (False, True), (True, False), (False, False)):
+        eng.add_rows, eng.enc_head_bf16 = knobs
+        with torch.no_grad():
+            outs[knobs] = [t.clone() for t in eng.forward(px)]
+    eng.add_rows, eng.enc_head_bf16 = True, True
+    ref = outs[(True, True)]
+    for knobs, (lg, bx) in outs.items():
+        assert torch.equal(lg, ref[0]) and torch.equal(bx, ref[1]), knobs
+
+
 def test_batch_equals_single(tmp_path):
     """bs=3 in one engine call gives the same per-image outputs as three bs=1 calls (bs1 GEMMs use
     split-K, so the fp32 summation order differs: compare at the parity bar, not bitwise)."""
