@@ -273,6 +273,11 @@ int sp_topk_rows(const float* x, int64_t ldx, int rows, int n, int reduce_c, int
  * (enc_outputs_class.max(-1).values, M2:1599), spread over the chip; sp_topk_rows(reduce_c = 1)
  * then ranks one key per anchor. */
 int sp_rowmax(const float* x, int64_t ldx, int64_t rows, int c, float* out, void* stream);
+/* ABI v15. out[r] = max_c (a[r, :] · w[c, :] + bias[c]), c < n: the bf16 variant's score head and its per-anchor
+ * class max in one pass (M2:1587-1599), equal bit for bit to sp_conv2d (SP_PREC_BF16, bf16 A rows) + sp_rowmax.
+ * a: bf16 rows [rows, lda], w: bf16 [n, k] (k contiguous), n <= 96, k = 256, 16-byte aligned. */
+int sp_linear_rowmax_bf16(const uint16_t* a, int64_t lda, const uint16_t* w, const float* bias, int rows, int n,
+                          int k, float* out, void* stream);
 /* dst[b, i, :] = src[b*src_rows + idx[b, i], :] */
 int sp_gather_rows(const float* src, int64_t ld_src, int src_rows, const int32_t* idx, int k,
                    int batch, int d, float* dst, int64_t ld_dst, void* stream);

@@ -126,6 +126,7 @@ _SIGS = {
     "sp_ref_init": (i32, [vp, i64, vp, vp, i32, i32, vp, vp]),
     "sp_box_refine": (i32, [vp, i64, vp, i32, vp]),
     "sp_add_rows": (i32, [vp, i64, vp, i64, vp, vp, i64, i32, i32, vp]),
+    "sp_linear_rowmax_bf16": (i32, [vp, i64, vp, vp, i32, i32, i32, vp, vp]),
     "sp_postprocess": (i32, [vp, vp, vp, i32, i32, i32, i32, f32, vp, vp, vp, vp, vp, vp]),
     "sp_jpeg_decode_coefs": (i32, [vp, i64, C.POINTER(SpJpegLayout), vp, i64]),
     "sp_jpeg_to_rgb": (i32, [vp, C.POINTER(SpJpegLayout), vp, i64, vp, i64, vp, vp]),

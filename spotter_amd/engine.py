@@ -216,6 +216,8 @@ class Engine:
         # the bf16 variant's encoder head LayerNorm written as bf16 rows for the score projection (decode); False =
         # the fp32 normalised map (A/B)
         self.enc_head_bf16 = True
+        # with it, the score head and its per-anchor class max fused (sp_linear_rowmax_bf16); False = GEMM + rowmax
+        self.enc_rowmax_fused = True
         self.dev = torch.device(device)
         if self.dev.type != "cuda":
             raise RuntimeError("spotter_amd runs on an MI355X (gfx950) device only")
@@ -862,7 +864,7 @@ class Engine:
         anchors, valid = self._const(("anchors", tuple(shapes)), lambda: tuple(
             _t(a, self.dev) for a in anchors_for(shapes)))
         rows = B * S
-        cls = self._buf("enc_cls", rows, NC)
+        cmax = self._buf("enc_cls_max", rows)
         lw = self.enc_output
         # the bf16 variant's score projection rounds its operand to bf16 anyway: the encoder head's LayerNorm
         # writes bf16 rows for it (half the write and the read of the normalised map), and the Q selected rows
@@ -875,14 +877,21 @@ class Engine:
                        **_wkw(lw.w16))
             om16 = self._buf("om16", rows, D, dtype=torch.int16)
             ops.layernorm(pre, *self.enc_ln, view(om16, D), rows, D, cfg.layer_norm_eps)
-            self._lin_op(view(om16, D), rows, self.enc_score, view(cls, NC))
+            sw = self.enc_score
+            if self.enc_rowmax_fused and NC <= 96 and sw.k == 256:
+                # the score head and its class max in one pass, bit-identical to the GEMM + sp_rowmax below
+                ops.linear_rowmax_bf16(view(om16, D), rows, sw.k, sw.w16, NC, sw.b, cmax)
+            else:
+                cls = self._buf("enc_cls", rows, NC)
+                self._lin_op(view(om16, D), rows, sw, view(cls, NC))
+                ops.rowmax(view(cls, NC), rows, NC, cmax)
         else:
             om = self._buf("om", rows, D)
+            cls = self._buf("enc_cls", rows, NC)
             self._lin_op(view(src, D), rows, lw, view(om, D), row_scale=valid, ln=self.enc_ln)
             self._lin_op(view(om, D), rows, self.enc_score, view(cls, NC))
+            ops.rowmax(view(cls, NC), rows, NC, cmax)
         topk = self._buf("topk", B, Q, dtype=torch.int32)
-        cmax = self._buf("enc_cls_max", rows)
-        ops.rowmax(view(cls, NC), rows, NC, cmax)
         ops.topk_rows(V(cmax, 0, S), B, S, Q, topk)
         Bq = B * Q
         h = self._buf("dec_h", Bq, D)

@@ -508,6 +508,17 @@ def rowmax(x: V, rows, c, out: torch.Tensor):
             0, 4 * rows * (c + 1), (rows, c))
 
 
+def linear_rowmax_bf16(x: V, rows: int, k: int, wt16: torch.Tensor, n: int, bias: torch.Tensor, out: torch.Tensor):
+    """out[r] = max_c (x[r] · W[c] + bias[c]) over n classes: bf16 rows x, bf16 weights [n, k] (the bf16 mode's
+    packed linear weights) — the score head + rowmax of query selection without the logits."""
+    xp = x.need(rows, k, "linear_rowmax.x", bf16=True)
+    if wt16.dtype != torch.int16 or wt16.numel() < n * k or out.numel() < rows or bias.numel() < n:
+        raise ValueError("linear_rowmax_bf16: weight / bias / out size")
+    _launch("conv", "sp_linear_rowmax_bf16", (xp, x.ld, wt16.data_ptr(), bias.data_ptr(), rows, n, k, out.data_ptr(),
+                                              stream()), 2 * rows * n * k, rows * k * 2 + n * k * 2 + rows * 4,
+            (rows, n, k, 1, 1, "bf16", "rows", "rowmax"))
+
+
 def gather_rows(src: V, src_rows, idx: torch.Tensor, k, batch, d, dst: V):
     sp_ = src.need(batch * src_rows, d, "gather.src")
     dp = dst.need(batch * k, d, "gather.dst")

@@ -1312,3 +1312,28 @@ def test_add_rows(dev, bf16):
     else:
         assert np.array_equal(got[:, :cols], want)
     assert not got[:, cols:].any()  # nothing written past the row
+
+
+@pytest.mark.parametrize("rows,n", [(1, 80), (129, 80), (5000, 91), (60000, 80), (777, 96), (300, 1)])
+def test_linear_rowmax_bf16_matches_gemm_then_rowmax(dev, rows, n):
+    """sp_linear_rowmax_bf16 (ABI v15: the bf16 variant's score head + class max, M2:1587-1599) equals the
+    bf16-mode GEMM on the same bf16 rows followed by sp_rowmax, bit for bit (same MFMA, k order and bias fma)."""
+    from spotter_amd import ops
+    from spotter_amd.ops import V, view
+
+    rng = np.random.default_rng(rows * 100 + n)
+    k, lda = 256, 264
+    x16, _ = _bf16_rows(rng.standard_normal((rows, lda)).astype(np.float32))
+    w = (rng.standard_normal((n, k)) / 16).astype(np.float32)
+    b = rng.standard_normal(n).astype(np.float32)
+    xt = V(T(x16.reshape(-1), dev), 0, lda)
+    wt = T(w.reshape(-1), dev)
+    w16 = T(ops.bf16_bits(w).view(np.int16).reshape(-1), dev)
+    bt = T(b, dev)
+    logits = torch.empty(rows * n, device=dev)
+    ops.linear(xt, rows, k, wt, n, view(logits, n), bias=bt, wt16=w16)
+    want = torch.empty(rows, device=dev)
+    ops.rowmax(view(logits, n), rows, n, want)
+    got = torch.full((rows,), float("nan"), device=dev)
+    ops.linear_rowmax_bf16(xt, rows, k, w16, n, bt, got)
+    assert torch.equal(got, want)

@@ -341,10 +341,11 @@ def test_two_stream_forward_is_deterministic():
 
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_operand_materialisations_are_bit_identical(precision):
-    """Engine.add_rows (h + pos materialised by sp_add_rows for the LDS-DMA tiles) and Engine.enc_head_bf16 (the
+    """Engine.add_rows (h + pos materialised by sp_add_rows for the LDS-DMA tiles), Engine.enc_head_bf16 (the
     bf16 variant's encoder-head LayerNorm into bf16 rows, decoder queries normalised from the gathered pre-norm
-    rows) change where operands are rounded or added, not their values: the logits and boxes equal the A2-addend /
-    fp32-map forms bit for bit (round 6)."""
+    rows) and Engine.enc_rowmax_fused (its score head + class max in one kernel) change where operands are
+    rounded, added or kept, not their values: the logits and boxes equal the A2-addend / fp32-map / GEMM + rowmax
+    forms bit for bit (round 6)."""
     import torch
 
     from spotter_amd import SpotterForObjectDetection, SpotterImageProcessor
@@ -355,12 +356,13 @@ def test_operand_materialisations_are_bit_identical(precision):
     px = SpotterImageProcessor()(images=(load_images(g) * 8)[:16], return_tensors="pt")["pixel_values"].to("cuda")
     eng = model.engine
     outs = {}
-    for knobs in ((True, True), (False, True), (True, False), (False, False)):
-        eng.add_rows, eng.enc_head_bf16 = knobs
+    for knobs in ((True, True, True), (False, True, True), (True, False, True), (False, False, True),
+                  (True, True, False)):
+        eng.add_rows, eng.enc_head_bf16, eng.enc_rowmax_fused = knobs
         with torch.no_grad():
             outs[knobs] = [t.clone() for t in eng.forward(px)]
-    eng.add_rows, eng.enc_head_bf16 = True, True
-    ref = outs[(True, True)]
+    eng.add_rows, eng.enc_head_bf16, eng.enc_rowmax_fused = True, True, True
+    ref = outs[(True, True, True)]
     for knobs, (lg, bx) in outs.items():
         assert torch.equal(lg, ref[0]) and torch.equal(bx, ref[1]), knobs
 
