@@ -101,10 +101,8 @@ extern "C" int sp_linear_rowmax_bf16(const uint16_t* a, int64_t lda, const uint1
                "sp_linear_rowmax_bf16: bad args (n <= %d, k = 256)", HM_NP);
   SP_ARG_CHECK(lda >= k && lda % 8 == 0 && ((uintptr_t)a & 15) == 0 && ((uintptr_t)w & 15) == 0,
                "sp_linear_rowmax_bf16: 16-byte aligned rows, lda %% 8 == 0");
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int nblk = (rows + 127) / 128;
-  const int grid = nblk < 2 * cus ? nblk : 2 * cus;
+  const int grid = nblk < 2 * g_num_cus ? nblk : 2 * g_num_cus;  // two workgroups per CU (66 KB of LDS each)
   hipLaunchKernelGGL(linear_rowmax_bf16_kernel<32>, dim3(grid), dim3(256), 0, as_stream(stream), a, lda, w, bias,
                      rows, n, out);
   return check_launch("sp_linear_rowmax_bf16");
