@@ -1,6 +1,7 @@
 #!/bin/bash
 # Same-box A/B of this tree against the round-start tree built under _abtree/ (git archive <commit> | tar -x -C
 # _abtree; python -m spotter_amd.build_ext there): C2 / C3 / C2-bf16 bench lines alternating, events off.
+# .gpurunignore drops ./_abtree by default: narrow it to ./_abtree/spotter_amd/_build for the run.
 set -euo pipefail
 OUT=${1:-gpurun_out/abtree}; mkdir -p $OUT
 B="python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --latency-iters 0 --no-events"
